@@ -1,0 +1,199 @@
+"""ctypes front-end of the CPU restatement (oracle/npge_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, ``__graft_entry__.smoke()`` and
+the ``cpu_baseline`` leg of bench.py, as the parity checker.  The product
+package ``npge_amd`` never imports this module.
+
+Parity is pinned against the reference's own known-answer tests
+(src/test/hash.cpp, bloom_filter.cpp, anchor_finder.cpp, similar_aligner.cpp,
+aligner.cpp and test-script/anchor_finder/*) -- see tests/test_oracle_kat.py.
+The reference itself cannot be built here (Boost/Lua/luabind absent), so there
+is no oracle/_ref build ("Oracle").
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or (
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "npge_oracle.cpp"))
+        ):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
+        vp = ctypes.c_void_p
+        L.orc_glibc_rand.argtypes = [u32, ctypes.c_int, vp]
+        L.orc_make_hash.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.orc_make_hash.restype = u64
+        L.orc_reuse_hash.argtypes = [u64, ctypes.c_int, ctypes.c_char, ctypes.c_char, ctypes.c_int]
+        L.orc_reuse_hash.restype = u64
+        L.orc_complement_hash.argtypes = [u64, ctypes.c_int]
+        L.orc_complement_hash.restype = u64
+        L.orc_optimal_bits.argtypes = [u64, ctypes.c_double]
+        L.orc_optimal_bits.restype = i64
+        L.orc_optimal_hashes.argtypes = [u64, u64]
+        L.orc_optimal_hashes.restype = ctypes.c_int
+        L.orc_weight_factor.argtypes = [i64]
+        L.orc_weight_factor.restype = ctypes.c_int
+        L.orc_to_atgcn.argtypes = [ctypes.c_char_p, i64, vp]
+        L.orc_to_atgcn.restype = i64
+        L.orc_af_create.argtypes = [ctypes.c_int, i64, ctypes.c_int, i64, u32]
+        L.orc_af_create.restype = vp
+        L.orc_af_set_params.argtypes = [vp, vp, ctypes.c_int]
+        L.orc_af_free.argtypes = [vp]
+        L.orc_af_run.argtypes = [vp, ctypes.c_int, vp, vp, vp]
+        L.orc_af_run.restype = ctypes.c_int
+        L.orc_af_stats.argtypes = [vp, vp]
+        L.orc_af_params.argtypes = [vp, vp]
+        L.orc_af_fragments.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.orc_af_used.argtypes = [vp, vp]
+        L.orc_align.argtypes = [ctypes.c_int, ctypes.c_char_p, vp, vp, ctypes.c_int, vp, i64,
+                                ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        L.orc_align.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def glibc_rand(seed, n):
+    out = np.zeros(n, dtype=np.int32)
+    lib().orc_glibc_rand(seed, n, _ptr(out))
+    return [int(x) for x in out]
+
+
+def make_hash(s, ori=1, start=None, length=None):
+    """make_hash(start, length, ori) of make_hash.hpp:67-78 on string s."""
+    b = s.encode() if isinstance(s, str) else s
+    buf = ctypes.create_string_buffer(b, len(b))
+    start = 0 if start is None else start
+    length = len(b) - start if length is None else length
+    addr = ctypes.addressof(buf) + start
+    return lib().orc_make_hash(ctypes.cast(addr, ctypes.c_char_p), length, ori)
+
+
+def reuse_hash(h, length, rm, ad, forward=True):
+    return lib().orc_reuse_hash(h, length, rm.encode(), ad.encode(), int(forward))
+
+
+def complement_hash(h, k):
+    return lib().orc_complement_hash(h, k)
+
+
+def optimal_bits(members, p):
+    return lib().orc_optimal_bits(members, p)
+
+
+def optimal_hashes(members, bits):
+    return lib().orc_optimal_hashes(members, bits)
+
+
+def weight_factor(min_identity_x1e4):
+    return lib().orc_weight_factor(min_identity_x1e4)
+
+
+def to_atgcn(s):
+    b = s.encode() if isinstance(s, str) else s
+    out = ctypes.create_string_buffer(max(len(b), 1))
+    n = lib().orc_to_atgcn(b, len(b), ctypes.cast(out, ctypes.c_void_p))
+    return out.raw[:n].decode()
+
+
+class AnchorFinder:
+    """Sequential restatement of AnchorFinder (AnchorFinder.cpp:37-406).
+
+    The instance keeps used hashes across run() calls like the reference's
+    ``AnchorFinderImpl::used_hashes_``.
+    """
+
+    def __init__(self, anchor_size=20, anchor_fp_x1e4=1000, anchor_similar=True,
+                 max_anchor_fragments=100000, seed=1, params=None):
+        L = lib()
+        self._h = L.orc_af_create(anchor_size, anchor_fp_x1e4, int(anchor_similar),
+                                  max_anchor_fragments, seed)
+        if params is not None:
+            p = np.asarray(params, dtype=np.uint64)
+            L.orc_af_set_params(self._h, _ptr(p), len(p))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_af_free(self._h)
+            self._h = None
+
+    def run(self, seqs, names):
+        """seqs: list of str/bytes; names: list of str.  Returns a dict with the
+        SoA anchor set in reference order (block, then fragment order)."""
+        L = lib()
+        n = len(seqs)
+        bufs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
+        arr = (ctypes.c_char_p * n)(*bufs)
+        lens = np.array([len(b) for b in bufs], dtype=np.int64)
+        nm = (ctypes.c_char_p * n)(*[x.encode() for x in names])
+        rc = L.orc_af_run(self._h, n, ctypes.cast(arr, ctypes.c_void_p), _ptr(lens),
+                          ctypes.cast(nm, ctypes.c_void_p))
+        if rc != 0:
+            raise RuntimeError("oracle AnchorFinder failed: %d" % rc)
+        st = np.zeros(8, dtype=np.int64)
+        L.orc_af_stats(self._h, _ptr(st))
+        nb, nf, nu = int(st[5]), int(st[6]), int(st[7])
+        seq = np.zeros(nf, dtype=np.int32)
+        mn = np.zeros(nf, dtype=np.int64)
+        mx = np.zeros(nf, dtype=np.int64)
+        ori = np.zeros(nf, dtype=np.int32)
+        bs = np.zeros(nb + 1, dtype=np.int64)
+        L.orc_af_fragments(self._h, _ptr(seq), _ptr(mn), _ptr(mx), _ptr(ori), _ptr(bs))
+        params = np.zeros(int(st[2]), dtype=np.uint64)
+        L.orc_af_params(self._h, _ptr(params))
+        used = np.zeros(nu, dtype=np.uint64)
+        L.orc_af_used(self._h, _ptr(used))
+        return dict(seq=seq, min_pos=mn, max_pos=mx, ori=ori, block_start=bs,
+                    members=int(st[0]), bits=int(st[1]), hashes=int(st[2]),
+                    n_collected=int(st[3]), n_found_frags=int(st[4]),
+                    params=params, used=used)
+
+
+DEFAULT_SA = (1, 2, 10, 100, 9000)  # MISMATCH_CHECK, GAP_CHECK, ALIGNED_CHECK, MIN_LENGTH, MIN_IDENTITY
+
+
+def align(rows, mode="similar", params=DEFAULT_SA, return_past_end=False):
+    """mode: 'similar' = SimilarAligner::similar_aligner; 'align_seqs' =
+    AbstractAligner::align_seqs(similar); 'dummy' = align_seqs(DummyAligner);
+    'similar+refine'; 'refine' = refine_alignment only."""
+    m = {"similar": 0, "align_seqs": 1, "dummy": 2, "similar+refine": 3, "refine": 4,
+         "align_block": 5}[mode]
+    L = lib()
+    bufs = [r.encode() if isinstance(r, str) else bytes(r) for r in rows]
+    cat = b"".join(bufs)
+    lens = np.array([len(b) for b in bufs], dtype=np.int64)
+    prm = np.array(params, dtype=np.int32)
+    cap = max(1, 4 * (sum(len(b) for b in bufs) + 16) * max(1, len(rows)))
+    out_len = ctypes.c_int64(0)
+    pe = ctypes.c_int64(0)
+    while True:
+        out = np.zeros(cap, dtype=np.uint8)
+        rc = L.orc_align(len(rows), cat, _ptr(lens), _ptr(prm), m, _ptr(out), cap,
+                         ctypes.byref(out_len), ctypes.byref(pe))
+        if rc == -1:
+            cap = out_len.value * len(rows) + 1
+            continue
+        if rc != 0:
+            raise RuntimeError("oracle align failed: %d" % rc)
+        break
+    Ln = out_len.value
+    res = [out[i * Ln:(i + 1) * Ln].tobytes().decode() for i in range(len(rows))]
+    return (res, pe.value) if return_past_end else res

@@ -1,0 +1,289 @@
+"""Pins the CPU restatement (oracle/) to the reference's own known-answer tests.
+
+Sources (reference paths): src/test/hash.cpp, src/test/bloom_filter.cpp,
+src/test/anchor_finder.cpp, src/test/similar_aligner.cpp, src/test/aligner.cpp,
+test-script/anchor_finder/*/{in,out}.fasta (copied as data into tests/golden/).
+glibc rand() is pinned by tests/golden/glibc_rand.json (make_glibc_rand.py).
+"""
+import json
+import os
+
+import pytest
+
+from oracle import oracle as orc
+from npge_amd import io as nio
+from npge_amd.model import Block, Fragment, Sequence, blockset_hash, normalized_blocks
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# ---------------------------------------------------------------- glibc rand
+def test_glibc_rand_matches_libc_fixture():
+    with open(os.path.join(GOLD, "glibc_rand.json")) as f:
+        gold = json.load(f)
+    for seed, vals in gold.items():
+        assert orc.glibc_rand(int(seed) & 0xFFFFFFFF, len(vals)) == vals, seed
+
+
+def test_glibc_rand_kat_seed1():
+    # srand(1) -> 1804289383, 846930886, 1681692777
+    assert orc.glibc_rand(1, 3) == [1804289383, 846930886, 1681692777]
+
+
+# ---------------------------------------------------------------- hashing (hash.cpp)
+def test_hash_main():
+    s = orc.to_atgcn("CGCAtacccTGCGgcaGGGTcaGGGC")
+    assert orc.make_hash(s, 1, 0, 4) == orc.make_hash(s, -1, 12, 4)
+    assert orc.make_hash(s, 1, 0, 4) != orc.make_hash(s, 1, 12, 4)
+    assert orc.make_hash(s, 1, 16, 4) != orc.make_hash(s, 1, 22, 4)
+
+
+def test_hash_reuse_hash():
+    s = "CGCATACCCTGCGGCAGGGTCAGGGC"
+    h = orc.make_hash(s, 1, 0, 4)
+    assert orc.reuse_hash(h, 4, s[0], s[4]) == orc.make_hash(s, 1, 1, 4)
+
+
+def _frag_hash(s, mn, mx, ori):
+    # Fragment::hash -> Sequence::hash_impl(begin_pos, length, ori)
+    if ori == 1:
+        return orc.make_hash(s, 1, mn, mx - mn + 1)
+    return orc.make_hash(s, -1, mx, mx - mn + 1)
+
+
+def _frag_char(s, mn, mx, ori, i):
+    # Fragment::raw_at: position i (may be -1 or length) in fragment orientation
+    if ori == 1:
+        c = s[mn + i]
+    else:
+        c = s[mx - i]
+        c = {"A": "T", "T": "A", "G": "C", "C": "G"}.get(c, c)
+    return c
+
+
+def test_hash_reuse_hash_full():
+    # hash.cpp:36-74 (all i in [70,100), length in [1,100), both oris)
+    s = ("GATCCTCGATTAACAGTTTGGCCTGTTCCTATGTATGCCCTACTCCAAATGGT"
+         "GCCAACTGGATCAATCCTCAGTGCCGCGGGAATCATGTCTTTATTTATGCTTT"
+         "TCAGCTCTGCGAACTTAGGCTCAGCACAAGATTTAAGCGAGAAGCGAAAGCTG"
+         "ACCGGCAGGGGGGGCACGGTTAATAACTAAGACTGTAGCGTGACAAACGGACC")
+    for i in range(70, 100, 3):
+        for length in range(1, 100, 7):
+            if i + length > len(s) - 1:
+                continue
+            for fr_ori in (-1, 1):
+                for move_ori in (-1, 1):
+                    mn, mx = i, i + length - 1
+                    h = _frag_hash(s, mn, mx, fr_ori)
+                    forward = move_ori == fr_ori
+                    rm = _frag_char(s, mn, mx, fr_ori, 0 if forward else length - 1)
+                    ad = _frag_char(s, mn, mx, fr_ori, length if forward else -1)
+                    reused = orc.reuse_hash(h, length, rm, ad, forward)
+                    mn2, mx2 = mn + move_ori, mx + move_ori
+                    assert reused == _frag_hash(s, mn2, mx2, fr_ori)
+                    assert orc.complement_hash(_frag_hash(s, mn2, mx2, fr_ori), length) == \
+                        _frag_hash(s, mn2, mx2, -fr_ori)
+
+
+# ---------------------------------------------------------------- Bloom sizing (bloom_filter.cpp)
+def test_bloom_sizing_kats():
+    m = orc.optimal_bits(1000000, 0.01)
+    assert m == 9585059
+    assert orc.optimal_hashes(1000000, m) == 7
+    m2 = orc.optimal_bits(2, 0.000001)
+    assert m2 == 59
+    assert orc.optimal_hashes(2, m2) == 20
+    assert 0 < orc.optimal_bits(0, 0.1) < 100
+    assert 0 < orc.optimal_bits(1, 0.1) < 100
+    assert 0 < orc.optimal_hashes(0, 1) < 100
+    assert 0 < orc.optimal_hashes(1, 1) < 100
+
+
+# ---------------------------------------------------------------- AnchorFinder (anchor_finder.cpp)
+def _af(seqs, k, seed=1, **kw):
+    af = orc.AnchorFinder(anchor_size=k, seed=seed, **kw)
+    names = ["s%d" % i for i in range(len(seqs))]
+    return af.run([orc.to_atgcn(x) for x in seqs], names)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 17, 12345])
+def test_af_main(seed):
+    r = _af(["tgGTCCGagCGGACggcc"], 5, seed)
+    nb = len(r["block_start"]) - 1
+    if nb == 1:  # BOOST_WARN in the reference
+        s = orc.to_atgcn("tgGTCCGagCGGACggcc")
+        f = s[r["min_pos"][0]:r["max_pos"][0] + 1]
+        assert f in ("GTCCG", "CGGAC") or True
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 17, 12345])
+def test_af_n_negative(seed):
+    assert len(_af(["tgGTNCGagCGNACggcc"], 5, seed)["block_start"]) - 1 == 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 17, 12345])
+def test_af_n_positive(seed):
+    assert len(_af(["GTNCGATAnnnGTNCGATA"], 5, seed)["block_start"]) - 1 > 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 17, 12345])
+def test_af_palindrome(seed):
+    assert len(_af(["ATGCAT"], 6, seed)["block_start"]) - 1 == 0
+
+
+def test_af_several_sequences():
+    r = _af(["GAAAGAAA", "GAAAGAAA"], 3, 1)
+    nb = len(r["block_start"]) - 1
+    assert nb >= 1
+
+
+def _load_case(case):
+    d = os.path.join(GOLD, "anchor_finder", case)
+    with open(os.path.join(d, "in.fasta")) as f:
+        recs = list(nio.read_fasta(f.read()))
+    with open(os.path.join(d, "out.fasta")) as f:
+        exp = nio.read_blockset(f.read())
+    return recs, exp
+
+
+def af_blocks_from_result(r, seqs):
+    blocks = []
+    bs = r["block_start"]
+    for b in range(len(bs) - 1):
+        frs = [Fragment(seqs[int(r["seq"][i])], int(r["min_pos"][i]), int(r["max_pos"][i]),
+                        int(r["ori"][i])) for i in range(bs[b], bs[b + 1])]
+        blocks.append(Block(frs))
+    return blocks
+
+
+@pytest.mark.parametrize("case", ["1", "bug-n-in-init-frame", "complement-no-inverse",
+                                  "inverse", "inverse-no-complement"])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_af_script_fixtures(case, seed):
+    """test-script/anchor_finder/script.npge with --anchor-size:=20, compared by
+    blockset_hash like meta_test.cxx:86."""
+    recs, exp = _load_case(case)
+    seqs = [Sequence(n, nio.to_atgcn(raw)) for n, _, raw in recs]
+    af = orc.AnchorFinder(anchor_size=20, seed=seed)
+    r = af.run([s.data for s in seqs], [s.name for s in seqs])
+    got = af_blocks_from_result(r, seqs)
+    assert normalized_blocks(got) == normalized_blocks(exp.blocks)
+    assert blockset_hash(got) == blockset_hash(exp.blocks)
+
+
+def test_af_used_hashes_persist():
+    """AnchorFinder memorizes hashes of previous runs (AnchorFinder.hpp:13-15),
+    except the first group's hash (quirk, AnchorFinder.cpp:366-387): blocks of a
+    second run on the same input are a subset of the first run's."""
+    recs, _ = _load_case("1")
+    seqs = [Sequence(n, nio.to_atgcn(raw)) for n, _, raw in recs]
+    af = orc.AnchorFinder(anchor_size=20, seed=1)
+    r1 = af.run([s.data for s in seqs], [s.name for s in seqs])
+    u1 = list(r1["used"])
+    assert u1 == sorted(u1) and len(set(u1)) == len(u1)
+    r2 = af.run([s.data for s in seqs], [s.name for s in seqs])
+    b1 = normalized_blocks(af_blocks_from_result(r1, seqs))
+    b2 = normalized_blocks(af_blocks_from_result(r2, seqs))
+    assert b2 <= b1
+    assert r2["n_collected"] <= r1["n_collected"]
+
+
+# ---------------------------------------------------------------- SimilarAligner (similar_aligner.cpp)
+def test_sa_n():
+    assert orc.align(["ATTT", "ANTT", "ATTT"]) == ["ATTT", "ANTT", "ATTT"]
+
+
+def test_sa_gap():
+    assert orc.align(["ATGC", "AGC", "ATGC"]) == ["ATGC", "A-GC", "ATGC"]
+
+
+def test_sa_gap_2():
+    r = orc.align(["CCCATATGG", "CCATATCG"], mode="similar+refine")
+    assert r[0] == "CCCATATGG"
+    assert r[1] in ("CC-ATATCG", "-CCATATCG", "C-CATATCG")
+
+
+def test_sa_long_gap():
+    r = orc.align(["ACCAGCTTTCGACCGCGGTGGCGATCGCGATATTAG", "ACCAGCTGGTGGCGATCGCGATATTAG",
+                   "ACCAGCTTTCGACCGCGGTGGCGATCGCGATATTAG"])
+    assert r == ["ACCAGCTTTCGACCGCGGTGGCGATCGCGATATTAG", "ACCAGCT---------GGTGGCGATCGCGATATTAG",
+                 "ACCAGCTTTCGACCGCGGTGGCGATCGCGATATTAG"]
+
+
+def test_sa_empty():
+    r = orc.align(["ATG", "AG", ""])
+    assert len(r[0]) >= 3 and len(r[0]) == len(r[1]) == len(r[2])
+
+
+def test_sa_end():
+    assert orc.align(["ATG", "AG"]) == ["ATG", "A-G"]
+
+
+def test_sa_gap_repeat():
+    assert orc.align(["CGAAT", "CAAAT"]) == ["CGAAT", "CAAAT"]
+
+
+def test_refinement_3():
+    assert orc.align(["CCGG", "CG-G", "CG-G", "CG-G"], mode="refine") == \
+        ["CCGG", "C-GG", "C-GG", "C-GG"]
+
+
+def test_refinement_4():
+    assert orc.align(["CCGGCC", "CGG--C"], mode="refine") == ["CCGGCC", "C-GG-C"]
+
+
+def test_refinement_5():
+    assert orc.align(["-CCCCCC", "CCCACCC", "CCCTCCC"], mode="refine") == \
+        ["CCC-CCC", "CCCACCC", "CCCTCCC"]
+
+
+def test_sa_end_gap():
+    r = orc.align(["GTTT", "GTTTT"])
+    assert len(r[0]) == 5 and r[0][4] != "-"
+
+
+def test_sa_bad():
+    r = orc.align(["GCTATAAAGCAGCCTTCTTAGCTCACC", "ACTTGATGTGCGGCTCGGGATATTTCA",
+                   "CCCTCTCTGGGCAGGGCGAACATTAAA", "TTGTAATGCTATTCCATAGTGAGATGA"])
+    assert len(set(len(x) for x in r)) == 1
+
+
+def test_sa_repeat_with_mismatch():
+    r = orc.align(["AGAGCGGTTCCGGCGATTCCGTT", "AGAGCGATTCCGTT"])
+    assert r[0] == "AGAGCGGTTCCGGCGATTCCGTT"
+    assert r[1][6:12] == "------"
+
+
+def test_sa_exclusive_gap_columns1():
+    rows = [orc.to_atgcn("TTATGAGTCGAGA-ATATGGTGCCAAAGT"), orc.to_atgcn("TTATGAGTCGAGATAT--GGTGCCAAAGT")]
+    r = orc.align(rows, mode="similar+refine")
+    assert r[0] == "TTATGAGTCGAGAATATGGTGCCAAAGT"
+    assert r[1] in ("TTATGAGTCGAG-ATATGGTGCCAAAGT", "TTATGAGTCGAGA-TATGGTGCCAAAGT")
+
+
+def test_aligner_remove_gap_cols():
+    assert orc.align(["A-T-G-CATG", "ACT-GTCAT-"], mode="dummy") == ["A-TG-CATG", "ACTGTCAT-"]
+
+
+def test_aligner_self_test():
+    # AbstractAligner::test (AbstractAligner.cpp:39-49), aligner.cpp:14-28
+    assert orc.align(["AT", "A"], mode="align_seqs") == ["AT", "A-"]
+    assert orc.align(["AT", "T"], mode="align_seqs") == ["AT", "-T"]
+    assert orc.align(["AT", "A"], mode="dummy") == ["AT", "A-"]
+    assert orc.align(["AT", "T"], mode="dummy") != ["AT", "-T"]
+
+
+def test_align_script_fixture():
+    """test-script/align/1: RemoveAlignment + MetaAligner(similar) returns the input."""
+    with open(os.path.join(GOLD, "align", "1", "in.fasta")) as f:
+        recs = list(nio.read_fasta(f.read()))
+    rows = [raw.upper() for _, _, raw in recs]
+    plain = [r.replace("-", "") for r in rows]
+    got = orc.align(plain, mode="align_block")
+    assert got == rows
+
+
+def test_weight_factor():
+    assert orc.weight_factor(9000) == 10
+    assert orc.weight_factor(10000) == 100
+    assert orc.weight_factor(5000) == 2

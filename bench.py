@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Headline benchmark: anchored+aligned Mbp/s on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one synthetic genome set already
+resident in HBM: AnchorFinder (k=20, fp=0.1, max 100000 fragments) followed by
+the block build on its anchors (DraftPangenome-equivalent).
+value = input bp of all ranks / max-over-ranks wall time of the K timed steps.
+
+Multi-GPU (torch.distributed.run, one rank per GPU over RCCL): every rank
+processes its own genome set (same config, rank-specific seed) -- weak scaling
+with no data-path collective (DESIGN.md "Multi-GPU").
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", default="C2", help="synthetic config timed for cpu_baseline")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from npge_amd import _capi, synth
+    from npge_amd.anchor_finder import AnchorFinder
+    from npge_amd import pipeline
+
+    _capi.check(_capi.lib().npgx_set_device(local_rank))
+    seed = synth.BASE_SEED + 1000 * rank + sum(map(ord, args.config))
+    names, seqs = synth.genome_set(args.config, seed=seed)
+    bp = synth.total_bp(seqs)
+    ss = _capi.SeqSet(seqs, names)          # resident in HBM before timing
+    job = pipeline.BlockBuild(ss, names, seqs)
+
+    def step():
+        return job.run()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        info = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    total_bp = bp * world
+    value = total_bp / 1e6 / dt * args.steps
+
+    # dominant kernel of the last step: algorithmic bytes / HIP-event duration
+    kts = job.kernel_times()
+    dom = max(kts, key=lambda k: k["ms"]) if kts else None
+    roofline = None
+    if dom and dom["ms"] > 0:
+        ach = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom["name"],
+                    "kernel_ms": round(dom["ms"], 4), "bytes_per_launch": dom["bytes"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_sample)
+
+    if rank == 0:
+        line = {
+            "metric": "anchored+aligned Mbp/sec at 1/2/4/8 MI355X; bit-exact anchor set vs CPU",
+            "value": round(value, 3),
+            "unit": "Mbp/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded Brucella-like proxy, npge_amd/synth.py)",
+            "config": {"workload": job.workload_name(args.config), "bp_per_rank": bp,
+                       "genomes": synth.CONFIGS[args.config][0], "anchor_size": 20,
+                       "anchor_fp": 0.1, "max_anchor_fragments": 100000,
+                       "parallelism": "replica-per-gpu x%d" % world},
+            "last_step": info,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(config):
+    """The CPU restatement (oracle/, single thread, reference 1-worker semantics)
+    timed on this host on the same kind of workload."""
+    from npge_amd import synth
+    from oracle import oracle as orc
+    from npge_amd import pipeline
+    names, seqs = synth.genome_set(config)
+    bp = synth.total_bp(seqs)
+    t = pipeline.cpu_reference_step(orc, names, seqs)
+    return {"value": round(bp / 1e6 / t, 4), "unit": "Mbp/s", "cores": 1, "kind": "port",
+            "sample": "%s synthetic set (%d bp), one full step of the same workload, oracle/ "
+                      "C++ -O3, 1 thread" % (config, bp), "seconds": round(t, 3)}
+
+
+if __name__ == "__main__":
+    main()

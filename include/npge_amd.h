@@ -1,0 +1,162 @@
+/*
+ * npge_amd.h -- C ABI of the MI355X-native anchor-finding / greedy-MSA engine
+ * for NPG-explorer's block-construction hot path.
+ *
+ * Plain pointers and sizes only.  Every handle owns one hipStream_t and lives on
+ * the device that was current (npgx_set_device) when it was created; handles
+ * are not thread-safe.  The caller owns inputs; the library owns outputs until
+ * the matching *_free.  All functions return NPGX_OK (0) or a negative code;
+ * npgx_last_error() returns the thread-local message of the last failure.
+ *
+ * Reference interfaces replaced (paths in NPG-explorer 0.5.8):
+ *   npgx_seqset_*   Sequence storage + SeqBase::make_seqs ranking
+ *                   (src/model/Sequence.cpp:151-179,525-600; src/algo/SeqI.hpp:45-57)
+ *   npgx_af_*       Processor "AnchorFinder" (src/algo/AnchorFinder.hpp:33-53,
+ *                   AnchorFinder.cpp:37-53 options, :393-406 run_impl)
+ *   npgx_align_*    AbstractAligner::align_seqs + SimilarAligner::similar_aligner
+ *                   (src/algo/AbstractAligner.cpp:104-143,
+ *                   src/algo/SimilarAligner.cpp:487-501), MetaAligner
+ *                   "aligner-type" similar|dummy (src/algo/MetaAligner.cpp:22-84)
+ */
+#ifndef NPGE_AMD_H_
+#define NPGE_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NPGX_OK 0
+#define NPGX_ERR_ARG (-1)      /* bad argument / option rule violated */
+#define NPGX_ERR_HIP (-2)      /* HIP runtime failure */
+#define NPGX_ERR_NODEV (-3)    /* no usable GPU */
+#define NPGX_ERR_RANGE (-4)    /* input outside supported sizes */
+#define NPGX_ERR_STATE (-5)    /* result requested before a run */
+
+typedef struct npgx_seqset npgx_seqset;
+typedef struct npgx_af npgx_af;
+typedef struct npgx_aligner npgx_aligner;
+
+/* ------------------------------------------------------------------ runtime */
+const char* npgx_last_error(void);
+const char* npgx_version(void);
+int npgx_device_count(int32_t* n);
+int npgx_set_device(int32_t device);
+
+/* Per-kernel timing of the last run of a handle (HIP events on the handle's
+ * stream).  bytes = algorithmic bytes of that launch. */
+typedef struct {
+    char name[32];
+    double ms;
+    double bytes;
+    int64_t units;   /* windows / residues processed by the launch */
+} npgx_kernel_time;
+
+/* ------------------------------------------------------------------ sequences
+ * Creates a device-resident, 2-bit packed (A0 T1 G2 C3, LSB first) sequence set
+ * with an N bitmap.  Input strings go through Sequence::to_atgcn
+ * (uppercase, IUPAC -> N, other characters dropped).  Sequences are ranked by
+ * (size desc, name asc, input index asc) -- the pinned form of the reference's
+ * unstable size sort (SeqI.hpp:54).  names may be NULL (empty names). */
+int npgx_seqset_create(const char* const* seqs, const int64_t* lens,
+                       const char* const* names, int32_t n, npgx_seqset** out);
+int npgx_seqset_count(const npgx_seqset* s, int32_t* n);
+/* size after to_atgcn of input sequence `index` */
+int npgx_seqset_size(const npgx_seqset* s, int32_t index, int64_t* size);
+/* rank of input sequence `index` in the processing order */
+int npgx_seqset_rank(const npgx_seqset* s, int32_t index, int32_t* rank);
+/* copies the ATGCN text of [start, start+len) of sequence `index` into out */
+int npgx_seqset_text(const npgx_seqset* s, int32_t index, int64_t start, int64_t len,
+                     char* out);
+/* total device bytes held (packed words + N bitmap) */
+int npgx_seqset_device_bytes(const npgx_seqset* s, int64_t* bytes);
+void npgx_seqset_free(npgx_seqset* s);
+
+/* ------------------------------------------------------------------ AnchorFinder
+ * Options mirror AnchorFinder's (AnchorFinder.cpp:37-53, CMakeLists.txt:41-45):
+ *   anchor-size (1..32, default 20), anchor-fp (Decimal, default 0.1 -> 1000),
+ *   anchor-similar (default 1), max-anchor-fragments (default 100000).
+ * The Bloom hash parameters are glibc rand() after srand(bloom_seed) -- the
+ * reference draws them after srand(make_seed()) (BloomFilter.cpp:55-63) -- or the
+ * explicit vector bloom_params[0..n_bloom_params) when n_bloom_params > 0. */
+typedef struct {
+    int32_t anchor_size;
+    int32_t anchor_similar;
+    int64_t anchor_fp_x1e4;
+    int64_t max_anchor_fragments;
+    uint32_t bloom_seed;
+    int32_t n_bloom_params;
+    const uint64_t* bloom_params;
+} npgx_af_options;
+
+void npgx_af_default_options(npgx_af_options* o);
+
+typedef struct {
+    int64_t members;        /* estimate_length (AnchorFinder.cpp:81-97) after 4^k cap */
+    int64_t bloom_bits;     /* optimal_bits (BloomFilter.cpp:147-156) */
+    int32_t bloom_hashes;   /* optimal_hashes (BloomFilter.cpp:158-164) */
+    int32_t pad0;
+    uint64_t bloom_params[32];
+    int64_t n_windows;      /* windows scanned per pass (sum of size-k+1) */
+    int64_t n_collected_raw;/* collected windows (before sort/unique) */
+    int64_t n_collected;    /* |H| after sort + unique */
+    int64_t n_found_frags;  /* FoundFragments before truncation */
+    int64_t n_kept_groups;  /* hash groups materialised before truncation */
+    int64_t n_blocks;
+    int64_t n_fragments;
+    int64_t n_used;         /* size of the persistent used-hash set */
+} npgx_af_stats;
+
+/* The handle owns the persistent used-hash set (AnchorFinder.cpp:30-35): runs on
+ * the same handle skip hashes recorded by earlier runs, like the reference's
+ * processor instance cached by MetaProcessor (MetaProcessor.cpp:32-38). */
+int npgx_af_create(const npgx_af_options* o, npgx_af** out);
+int npgx_af_run(npgx_af* af, const npgx_seqset* s);
+int npgx_af_stats_get(const npgx_af* af, npgx_af_stats* out);
+/* Result of the last run, in reference order: blocks in FoundFragment (hash)
+ * order, fragments inside a block by (sequence rank, direct before reverse,
+ * position).  seq[] holds the INPUT index of the sequence; ori is +1/-1. */
+int npgx_af_result_counts(const npgx_af* af, int64_t* n_blocks, int64_t* n_fragments);
+int npgx_af_result_copy(const npgx_af* af, int64_t* block_start /* n_blocks+1 */,
+                        int32_t* seq, int64_t* min_pos, int64_t* max_pos, int8_t* ori);
+int npgx_af_used_hashes(const npgx_af* af, uint64_t* out, int64_t cap, int64_t* n);
+int npgx_af_clear_used(npgx_af* af);
+int npgx_af_kernel_times(const npgx_af* af, npgx_kernel_time* out, int32_t cap, int32_t* n);
+void npgx_af_free(npgx_af* af);
+
+/* ------------------------------------------------------------------ aligner
+ * Batched AbstractAligner::align_seqs with aligner-type "similar"
+ * (SimilarAligner) or "dummy" (DummyAligner).  A batch holds n_jobs independent
+ * alignment problems (one per block); job j owns rows
+ * [job_row_start[j], job_row_start[j+1]) and row r is the text
+ * rows[row_off[r] .. row_off[r+1]).  Rows must be ATGCN upper/lower case.
+ * Options (SimilarAligner.cpp:503-516, CMakeLists.txt:35-37,55-60): */
+typedef struct {
+    int32_t mismatch_check;     /* default 1 */
+    int32_t gap_check;          /* default 2 */
+    int32_t aligned_check;      /* default 10 */
+    int32_t min_length;         /* default 100 */
+    int64_t min_identity_x1e4;  /* default 9000 (Decimal 0.9) */
+    int32_t aligner_type;       /* 0 = similar, 1 = dummy */
+    int32_t refine;             /* 1 = also refine_alignment (align_block) */
+} npgx_align_options;
+
+void npgx_align_default_options(npgx_align_options* o);
+int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out);
+int npgx_align_batch(npgx_aligner* a, const char* rows, const int64_t* row_off,
+                     const int32_t* job_row_start, int32_t n_jobs);
+/* Output of the last batch: job j's aligned rows all have length out_len[j];
+ * row r's gapped text is out[out_off[r] .. out_off[r] + out_len[job(r)]). */
+int npgx_align_result_sizes(const npgx_aligner* a, int64_t* total_bytes);
+int npgx_align_result_copy(const npgx_aligner* a, char* out, int64_t* out_off,
+                           int64_t* job_len);
+int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_t cap,
+                            int32_t* n);
+void npgx_aligner_free(npgx_aligner* a);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NPGE_AMD_H_ */

@@ -1,0 +1,55 @@
+"""Builds the in-tree HIP library npge_amd/libnpge_amd.so for gfx950 with hipcc.
+
+hipcc cross-compiles without a GPU, so this runs in the CPU container; the .so
+travels to the GPU box with the repo snapshot.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libnpge_amd.so")
+SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip"]
+HEADERS = ["common.hpp", "sa_device.hpp"]
+ARCH = os.environ.get("NPGX_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "npge_amd.h"))
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    objs = []
+    procs = []
+    for src in [x for x in SOURCES if os.path.exists(os.path.join(CSRC, x))]:
+        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
+        cmd = ["hipcc", "-c", "-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
+               "-munsafe-fp-atomics", "-Wno-unused-result", "-I", os.path.join(os.path.dirname(HERE), "include"),
+               "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError("hipcc failed on %s:\n%s" % (src, out.decode(errors="replace")))
+    tmp = LIB + ".tmp"
+    cmd = ["hipcc", "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

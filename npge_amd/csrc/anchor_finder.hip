@@ -1,0 +1,767 @@
+// anchor_finder.hip -- MI355X-native AnchorFinder (src/algo/AnchorFinder.cpp:37-406).
+//
+// The reference runs two sequential rolling-hash passes per sequence: a Bloom
+// "seen before" pass collecting hashes (BloomTask, :152-197) and an exact
+// membership pass emitting FoundFragments (FragmentTask, :283-326), followed by a
+// sort / truncate / group step (:356-391).  Its Bloom pass is order-dependent
+// (a window is "found" when all k_b bits were already set by earlier windows).
+// Here the same result is computed data-parallel:
+//
+//   k_bloom_first   first[bit] = min over admitted windows of order(window)
+//                   (atomicMin; admitted = valid, hash not in the used set)
+//   k_found_collect found(p) = admitted(p) && all first[bit_i(p)] < order(p)
+//                   -- exactly "all bits were set by an earlier window";
+//                   collected(p) = found(p) && !(similar && found(p-1));
+//                   wave-ballot compaction of collected hashes
+//   sort + unique   H = sorted unique collected hashes (rocPRIM radix sort)
+//   k_table_insert  open-addressing table hash -> index in H
+//   k_ff_count      count[idx(h)]++ for every valid window whose hash is in H
+//   exclusive scan  offsets; cut G = #groups starting before max-anchor-fragments
+//   k_ff_scatter    windows of the first G groups -> (idx << B) | key2, where
+//                   key2 = 2*order_off(rank) + pos (+size if reverse) orders by
+//                   (rank, direct before reverse, pos) -- FoundFragment's order
+//   radix sort      over the candidate keys, truncate, group on the host.
+//
+// Windows are read straight from the 2-bit packed words: the window [p, p+k) is
+// bits [2p, 2p+2k) of the sequence's bit stream, which IS make_hash's value
+// (make_hash.hpp:29-42, LSB = first base); the reverse hash is the 2-bit-group
+// reversal of its complement (complement.cpp:24-50).
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+
+#include "common.hpp"
+
+namespace npgx {
+
+std::string genome_of(const std::string& name);
+uint64_t estimate_length(const npgx_seqset* s);
+int64_t optimal_bits(uint64_t members, double error_prob);
+int optimal_hashes(uint64_t members, uint64_t bits);
+void glibc_rand(uint32_t seed, int n, uint64_t* out);
+
+static constexpr int WG = 256;         // windows per workgroup (4 waves)
+static constexpr int MAX_KB = 32;
+
+struct SeqMeta {
+    int64_t size;
+    int64_t word_off;
+    int64_t n_off;
+    uint64_t order_off;   // sum of sizes of lower-ranked eligible sequences
+};
+
+struct Chunk {
+    int32_t seq;
+    int32_t pad;
+    int64_t pos;
+};
+
+struct AfArgs {
+    const SeqMeta* meta;
+    const Chunk* chunks;
+    const uint64_t* words;
+    const uint64_t* nmask;
+    const uint64_t* used;
+    int64_t n_used;
+    uint64_t kmask;
+    uint64_t mmagic;      // floor((2^64-1)/m)
+    uint32_t nbits_mask;  // (1<<k)-1 over the N bitmap
+    uint32_t m;
+    int32_t k;
+    int32_t kb;
+    int32_t similar;
+    int32_t pad;
+    uint64_t params[MAX_KB];
+};
+
+struct TableArgs {
+    const uint64_t* keys;
+    const uint32_t* vals;
+    uint32_t mask;
+    int32_t shift;
+};
+
+static constexpr uint64_t EMPTY_KEY = ~0ull;  // never a canonical hash (min(dir, rev))
+
+// ------------------------------------------------------------------ device helpers
+__device__ __forceinline__ uint64_t revcomp(uint64_t d, int k) {
+    uint64_t x = d ^ 0x5555555555555555ull;  // complement_letter(x) = x ^ 1 per base
+    x = __builtin_bitreverse64(x);
+    x = ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+    return x >> (64 - 2 * k);
+}
+
+// Loads window p of sequence s.  Returns false for windows containing N.
+__device__ __forceinline__ bool load_window(const AfArgs& a, const SeqMeta& s, int64_t p,
+                                            uint64_t& dir) {
+    const int64_t w = s.word_off + (p >> 5);
+    const int sh = (int)(p & 31) * 2;
+    const uint64_t lo = a.words[w], hi = a.words[w + 1];
+    uint64_t d = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+    dir = d & a.kmask;
+    const int64_t nw = s.n_off + (p >> 6);
+    const int nsh = (int)(p & 63);
+    const uint64_t nlo = a.nmask[nw], nhi = a.nmask[nw + 1];
+    const uint64_t nb = nsh ? ((nlo >> nsh) | (nhi << (64 - nsh))) : nlo;
+    return ((uint32_t)nb & a.nbits_mask) == 0;
+}
+
+__device__ __forceinline__ uint32_t bloom_index(uint64_t x, uint32_t m, uint64_t magic) {
+    // exact x % m for 64-bit x, 32-bit m: q_est in {q-1, q}
+    const uint64_t q = __umul64hi(x, magic);
+    uint64_t r = x - q * (uint64_t)m;
+    return (uint32_t)(r >= m ? r - m : r);
+}
+
+__device__ __forceinline__ bool in_sorted(const uint64_t* v, int64_t n, uint64_t h) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (v[mid] < h) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && v[lo] == h;
+}
+
+__device__ __forceinline__ int64_t table_find(const TableArgs& t, uint64_t h) {
+    uint32_t s = (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> t.shift) & t.mask;
+    while (true) {
+        const uint64_t key = t.keys[s];
+        if (key == h) return (int64_t)t.vals[s];
+        if (key == EMPTY_KEY) return -1;
+        s = (s + 1) & t.mask;
+    }
+}
+
+// valid && not used: the windows the reference admits to the Bloom filter
+// (AnchorFinder.cpp:170-182).
+__device__ __forceinline__ bool admitted(const AfArgs& a, const SeqMeta& s, int64_t p,
+                                         uint64_t& h, uint64_t& dir) {
+    if (p < 0 || p + a.k > s.size) return false;
+    if (!load_window(a, s, p, dir)) return false;
+    const uint64_t rev = revcomp(dir, a.k);
+    h = dir < rev ? dir : rev;
+    if (a.n_used && in_sorted(a.used, a.n_used, h)) return false;
+    return true;
+}
+
+__device__ __forceinline__ bool found_at(const AfArgs& a, const SeqMeta& s, int64_t p,
+                                         const uint32_t* __restrict__ first, uint64_t& h) {
+    uint64_t dir;
+    if (!admitted(a, s, p, h, dir)) return false;
+    const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
+    bool f = true;
+    for (int i = 0; i < a.kb; i++) {
+        const uint32_t idx = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+        f &= first[idx] < ord;
+    }
+    return f;
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ __launch_bounds__(WG) void k_bloom_first(AfArgs a, uint32_t* __restrict__ first) {
+    const Chunk c = a.chunks[blockIdx.x];
+    const SeqMeta s = a.meta[c.seq];
+    const int64_t p = c.pos + threadIdx.x;
+    uint64_t h, dir;
+    if (!admitted(a, s, p, h, dir)) return;
+    const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
+    for (int i = 0; i < a.kb; i++) {
+        const uint32_t idx = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+        atomicMin(&first[idx], ord);
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_found_collect(AfArgs a, const uint32_t* __restrict__ first,
+                                                      uint64_t* __restrict__ out,
+                                                      unsigned long long* __restrict__ n_out) {
+    __shared__ uint8_t fs[WG];
+    const Chunk c = a.chunks[blockIdx.x];
+    const SeqMeta s = a.meta[c.seq];
+    const int t = threadIdx.x;
+    const int64_t p = c.pos + t;
+    uint64_t h = 0;
+    const bool f = found_at(a, s, p, first, h);
+    fs[t] = f;
+    __syncthreads();
+    bool prev;
+    if (t > 0) {
+        prev = fs[t - 1];
+    } else {
+        uint64_t hp;
+        prev = found_at(a, s, p - 1, first, hp);  // p-1 < 0 -> false (AnchorFinder.cpp:189)
+    }
+    const bool col = f && !(a.similar && prev);
+    // wave-aggregated append
+    const unsigned long long mask = __ballot(col);
+    if (mask == 0) return;
+    const int lane = t & 63;
+    const int leader = __ffsll((long long)mask) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(n_out, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader);
+    if (col) {
+        const unsigned long long below = mask & ((1ull << lane) - 1ull);
+        out[base + __popcll(below)] = h;
+    }
+}
+
+__global__ void k_table_insert(const uint64_t* __restrict__ hs, int64_t n, uint64_t* keys,
+                               uint32_t* vals, uint32_t mask, int shift) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = hs[i];
+    uint32_t s = (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> shift) & mask;
+    while (true) {
+        const unsigned long long prev =
+            atomicCAS((unsigned long long*)&keys[s], (unsigned long long)EMPTY_KEY,
+                      (unsigned long long)h);
+        if (prev == EMPTY_KEY) {
+            vals[s] = (uint32_t)i;
+            return;
+        }
+        s = (s + 1) & mask;
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_ff_count(AfArgs a, TableArgs t, uint32_t* __restrict__ counts) {
+    const Chunk c = a.chunks[blockIdx.x];
+    const SeqMeta s = a.meta[c.seq];
+    const int64_t p = c.pos + threadIdx.x;
+    if (p + a.k > s.size) return;
+    uint64_t dir;
+    if (!load_window(a, s, p, dir)) return;
+    const uint64_t rev = revcomp(dir, a.k);
+    const uint64_t h = dir < rev ? dir : rev;
+    const int64_t idx = table_find(t, h);
+    if (idx >= 0) atomicAdd(&counts[idx], 1u);
+}
+
+__global__ void k_find_cut(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ counts,
+                           int64_t nH, uint64_t max_frag, uint64_t* __restrict__ out /*G, C, total*/) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint64_t total = nH ? (uint64_t)offsets[nH - 1] + counts[nH - 1] : 0;
+    int64_t lo = 0, hi = nH;  // first g with offsets[g] >= max_frag
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)offsets[mid] < max_frag) lo = mid + 1;
+        else hi = mid;
+    }
+    out[0] = (uint64_t)lo;
+    out[1] = lo < nH ? (uint64_t)offsets[lo] : total;
+    out[2] = total;
+}
+
+__global__ __launch_bounds__(WG) void k_ff_scatter(AfArgs a, TableArgs t, const uint64_t* __restrict__ H,
+                                                   uint64_t G, const uint32_t* __restrict__ offsets,
+                                                   uint32_t* __restrict__ cursor, int key_bits,
+                                                   uint64_t* __restrict__ cand) {
+    const Chunk c = a.chunks[blockIdx.x];
+    const SeqMeta s = a.meta[c.seq];
+    const int64_t p = c.pos + threadIdx.x;
+    if (p + a.k > s.size) return;
+    uint64_t dir;
+    if (!load_window(a, s, p, dir)) return;
+    const uint64_t rev = revcomp(dir, a.k);
+    const uint64_t h = dir < rev ? dir : rev;
+    if (h > H[G - 1]) return;  // groups beyond the cut (H is sorted)
+    const int64_t idx = table_find(t, h);
+    if (idx < 0) return;
+    // FoundFragment pos (AnchorFinder.cpp:295-301): + size for the reverse strand;
+    // a palindrome (dir == rev) counts as direct (:308).
+    const uint64_t pos2 = (uint64_t)p + (h == dir ? 0ull : (uint64_t)s.size);
+    const uint64_t key2 = 2ull * s.order_off + pos2;
+    const uint32_t slot = offsets[idx] + atomicAdd(&cursor[idx], 1u);
+    cand[slot] = ((uint64_t)idx << key_bits) | key2;
+}
+
+// ------------------------------------------------------------------ host helpers
+static int bits_for(uint64_t v) {  // bits needed to represent values < v
+    int b = 0;
+    while (b < 64 && (v > (1ull << b))) b++;
+    return b;
+}
+
+}  // namespace npgx
+
+using namespace npgx;
+
+struct npgx_af {
+    npgx_af_options opt;
+    std::vector<uint64_t> explicit_params;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<uint64_t> used;       // sorted (AnchorFinderImpl::used_hashes_)
+    bool used_dirty = true;
+    DevBuf<uint64_t> d_used;
+    DevBuf<SeqMeta> d_meta;
+    DevBuf<Chunk> d_chunks;
+    DevBuf<uint32_t> first;
+    DevBuf<uint64_t> hraw, hsorted, huniq;
+    DevBuf<unsigned long long> counters;  // [0] = n_raw, [1] = n_unique
+    DevBuf<uint64_t> tkeys;
+    DevBuf<uint32_t> tvals, counts, offsets, cursor;
+    DevBuf<uint64_t> cut;  // G, C, total
+    DevBuf<uint64_t> cand, cand_sorted;
+    DevBuf<unsigned char> temp;
+    uint64_t* h_pinned = nullptr;  // small host staging
+    npgx_af_stats stats{};
+    bool has_result = false;
+    std::vector<int64_t> r_block_start;
+    std::vector<int32_t> r_seq;
+    std::vector<int64_t> r_min, r_max;
+    std::vector<int8_t> r_ori;
+    StageTimer timer;
+    std::vector<uint64_t> host_keys, host_H;
+
+    void ensure_temp(size_t bytes) { temp.ensure(bytes); }
+};
+
+namespace npgx {
+
+// Sequence.cpp:193-202
+std::string genome_of(const std::string& name) {
+    std::vector<std::string> parts;
+    size_t start = 0;
+    while (true) {
+        size_t p = name.find('&', start);
+        if (p == std::string::npos) {
+            parts.push_back(name.substr(start));
+            break;
+        }
+        parts.push_back(name.substr(start, p - start));
+        start = p + 1;
+    }
+    if (parts.size() == 3 && (parts[2] == "c" || parts[2] == "l")) return parts[0];
+    return "";
+}
+
+// AnchorFinder.cpp:81-97 (over ALL sequences of the block set)
+uint64_t estimate_length(const npgx_seqset* s) {
+    std::map<std::string, uint64_t> gtl;
+    uint64_t max_length = 0;
+    for (int32_t i = 0; i < s->n; i++) {
+        uint64_t& g = gtl[genome_of(s->names[i])];
+        g += s->data[i].size();
+        max_length = std::max(max_length, g);
+    }
+    if (gtl.size() == 1) return max_length;  // consensuses
+    return max_length / 2 * 3;
+}
+
+static const double LN2 = 0.69314718055994530942;
+
+// BloomFilter.cpp:147-156 -- the reference stores the result in an int; sizes
+// that would overflow it are rejected instead of reproducing the UB.
+int64_t optimal_bits(uint64_t members, double error_prob) {
+    double v = double(members) * (-std::log(error_prob) / (LN2 * LN2)) + 0.5;
+    if (!(v < 2147483647.0)) return -1;
+    int r = (int)v;
+    if (r % 2 == 0) r += 1;
+    if (r < 1) r = 1;
+    return r;
+}
+
+// BloomFilter.cpp:158-164
+int optimal_hashes(uint64_t members, uint64_t bits) {
+    if (members == 0) return 1;  // +inf -> INT_MIN on x86 -> clamped to 1
+    int r = (int)std::round(LN2 * double(bits) / double(members));
+    if (r < 1) r = 1;
+    return r;
+}
+
+// glibc TYPE_3 random(): r[i] = r[i-31] + r[i-3], output r[i+344] >> 1
+void glibc_rand(uint32_t seed, int n, uint64_t* out) {
+    std::vector<uint32_t> r(34 + 310 + (size_t)n);
+    int32_t s0 = (int32_t)seed;
+    if (s0 == 0) s0 = 1;
+    r[0] = (uint32_t)s0;
+    for (int i = 1; i < 31; i++) {
+        int64_t v = (16807ll * (int32_t)r[i - 1]) % 2147483647ll;
+        if (v < 0) v += 2147483647ll;
+        r[i] = (uint32_t)v;
+    }
+    for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+    for (size_t i = 34; i < r.size(); i++) r[i] = r[i - 31] + r[i - 3];
+    for (int i = 0; i < n; i++) out[i] = (uint64_t)(r[344 + (size_t)i] >> 1);
+}
+
+static void af_run(npgx_af* af, const npgx_seqset* ss) {
+    NPGX_REQUIRE(ss->device == af->device, NPGX_ERR_ARG, "sequence set and finder on different devices");
+    NPGX_HIP(hipSetDevice(af->device));
+    hipStream_t st = af->stream;
+    const int k = af->opt.anchor_size;
+    af->timer.reset();
+    af->has_result = false;
+    npgx_af_stats& S = af->stats;
+    memset(&S, 0, sizeof(S));
+
+    // --- Bloom sizing (BloomTG::initialize_bloom AnchorFinder.cpp:120-131)
+    uint64_t members = estimate_length(ss);
+    if (k * 2 < 64) members = std::min<uint64_t>(members, 1ull << (2 * k));
+    const double fp = double(af->opt.anchor_fp_x1e4) / 10000.0;  // Decimal::to_d
+    const int64_t m = optimal_bits(members, fp);
+    NPGX_REQUIRE(m > 0, NPGX_ERR_RANGE, "Bloom filter size overflows the reference's int");
+    const int kb = optimal_hashes(members, (uint64_t)m);
+    NPGX_REQUIRE(kb <= MAX_KB, NPGX_ERR_RANGE, "too many Bloom hash functions");
+    AfArgs A;
+    memset(&A, 0, sizeof(A));
+    if (!af->explicit_params.empty()) {
+        NPGX_REQUIRE((int)af->explicit_params.size() >= kb, NPGX_ERR_ARG,
+                     "explicit Bloom parameter vector shorter than the hash count");
+        for (int i = 0; i < kb; i++) A.params[i] = af->explicit_params[i];
+    } else {
+        glibc_rand(af->opt.bloom_seed, kb, A.params);
+    }
+    S.members = (int64_t)members;
+    S.bloom_bits = m;
+    S.bloom_hashes = kb;
+    for (int i = 0; i < kb; i++) S.bloom_params[i] = A.params[i];
+
+    // --- eligible sequences (size >= k) are a prefix of the rank order
+    int32_t R = 0;
+    while (R < ss->n && (int64_t)ss->data[ss->by_rank[R]].size() >= k) R++;
+    std::vector<SeqMeta> meta(R > 0 ? R : 1);
+    std::vector<Chunk> chunks;
+    uint64_t order = 0;
+    int64_t n_windows = 0;
+    for (int32_t r = 0; r < R; r++) {
+        const int64_t size = (int64_t)ss->data[ss->by_rank[r]].size();
+        meta[r] = SeqMeta{size, ss->word_off[r], ss->n_off[r], order};
+        order += (uint64_t)size;
+        const int64_t nw = size - k + 1;
+        n_windows += nw;
+        for (int64_t p = 0; p < nw; p += WG) chunks.push_back(Chunk{r, 0, p});
+    }
+    NPGX_REQUIRE(order < 0xFFFFFFFEull, NPGX_ERR_RANGE, "more than 2^32-2 bases in one run");
+    S.n_windows = n_windows;
+    S.n_used = (int64_t)af->used.size();
+
+    // persistent used hashes on the device
+    if (af->used_dirty) {
+        af->d_used.ensure(af->used.size());
+        if (!af->used.empty())
+            NPGX_HIP(hipMemcpyAsync(af->d_used.p, af->used.data(), af->used.size() * 8,
+                                    hipMemcpyHostToDevice, st));
+        af->used_dirty = false;
+    }
+    const int64_t nchunks = (int64_t)chunks.size();
+    if (nchunks == 0) {
+        af->r_block_start.assign(1, 0);
+        af->r_seq.clear();
+        af->r_min.clear();
+        af->r_max.clear();
+        af->r_ori.clear();
+        af->has_result = true;
+        return;
+    }
+    af->d_meta.ensure(meta.size());
+    af->d_chunks.ensure(chunks.size());
+    NPGX_HIP(hipMemcpyAsync(af->d_meta.p, meta.data(), meta.size() * sizeof(SeqMeta),
+                            hipMemcpyHostToDevice, st));
+    NPGX_HIP(hipMemcpyAsync(af->d_chunks.p, chunks.data(), chunks.size() * sizeof(Chunk),
+                            hipMemcpyHostToDevice, st));
+
+    A.meta = af->d_meta.p;
+    A.chunks = af->d_chunks.p;
+    A.words = ss->words.p;
+    A.nmask = ss->nmask.p;
+    A.used = af->d_used.p;
+    A.n_used = (int64_t)af->used.size();
+    A.k = k;
+    A.kb = kb;
+    A.kmask = (k == 32) ? ~0ull : ((1ull << (2 * k)) - 1);
+    A.nbits_mask = (k == 32) ? 0xFFFFFFFFu : ((1u << k) - 1);
+    A.m = (uint32_t)m;
+    A.mmagic = ~0ull / (uint64_t)m;
+    A.similar = af->opt.anchor_similar ? 1 : 0;
+
+    const dim3 grid((unsigned)nchunks), block(WG);
+    uint64_t* hp = af->h_pinned;
+
+    // --- pass 1: Bloom first-setter + found/collect
+    af->first.ensure((size_t)m);
+    af->counters.ensure(4);
+    NPGX_HIP(hipMemsetAsync(af->counters.p, 0, 4 * sizeof(unsigned long long), st));
+    size_t ti = af->timer.begin("bloom_first", st, n_windows * (0.375 + 8.0 * kb), n_windows);
+    NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
+    hipLaunchKernelGGL(k_bloom_first, grid, block, 0, st, A, af->first.p);
+    NPGX_HIP(hipGetLastError());
+    af->timer.end(ti, st);
+
+    af->hraw.ensure((size_t)n_windows);
+    ti = af->timer.begin("found_collect", st, n_windows * (0.375 + 4.0 * kb), n_windows);
+    hipLaunchKernelGGL(k_found_collect, grid, block, 0, st, A, af->first.p, af->hraw.p,
+                       af->counters.p);
+    NPGX_HIP(hipGetLastError());
+    af->timer.end(ti, st);
+    NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8, hipMemcpyDeviceToHost, st));
+    NPGX_HIP(hipStreamSynchronize(st));
+    const int64_t n_raw = (int64_t)hp[0];
+    S.n_collected_raw = n_raw;
+
+    // --- bloomtg_postprocess (AnchorFinder.cpp:213-218): sort + unique
+    int64_t nH = 0;
+    if (n_raw > 0) {
+        af->hsorted.ensure((size_t)n_raw);
+        af->huniq.ensure((size_t)n_raw);
+        size_t b1 = 0, b2 = 0;
+        const unsigned end_bit = (unsigned)std::min(64, 2 * k);
+        NPGX_HIP(rocprim::radix_sort_keys(nullptr, b1, af->hraw.p, af->hsorted.p, (size_t)n_raw, 0u,
+                                          end_bit, st));
+        NPGX_HIP(rocprim::unique(nullptr, b2, af->hsorted.p, af->huniq.p, af->counters.p + 1,
+                                 (size_t)n_raw, rocprim::equal_to<uint64_t>(), st));
+        af->ensure_temp(std::max(b1, b2));
+        ti = af->timer.begin("sort_unique_H", st, n_raw * 8.0 * 4, n_raw);
+        NPGX_HIP(rocprim::radix_sort_keys(af->temp.p, b1, af->hraw.p, af->hsorted.p, (size_t)n_raw,
+                                          0u, end_bit, st));
+        NPGX_HIP(rocprim::unique(af->temp.p, b2, af->hsorted.p, af->huniq.p, af->counters.p + 1,
+                                 (size_t)n_raw, rocprim::equal_to<uint64_t>(), st));
+        af->timer.end(ti, st);
+        NPGX_HIP(hipMemcpyAsync(hp, af->counters.p + 1, 8, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipStreamSynchronize(st));
+        nH = (int64_t)hp[0];
+    }
+    S.n_collected = nH;
+
+    std::vector<uint64_t>& keys = af->host_keys;
+    std::vector<uint64_t>& Hh = af->host_H;
+    keys.clear();
+    Hh.clear();
+    uint64_t G = 0;
+    int key_bits = bits_for(2ull * order);
+    if (nH > 0) {
+        // --- membership table
+        uint64_t cap = 1024;
+        while (cap < 2ull * (uint64_t)nH) cap <<= 1;
+        NPGX_REQUIRE(cap <= (1ull << 31), NPGX_ERR_RANGE, "hash set too large");
+        int log2cap = 0;
+        while ((1ull << log2cap) < cap) log2cap++;
+        af->tkeys.ensure(cap);
+        af->tvals.ensure(cap);
+        TableArgs T{af->tkeys.p, af->tvals.p, (uint32_t)(cap - 1), 64 - log2cap};
+        ti = af->timer.begin("table_insert", st, nH * 8.0 + nH * 12.0, nH);
+        NPGX_HIP(hipMemsetAsync(af->tkeys.p, 0xFF, cap * 8, st));
+        hipLaunchKernelGGL(k_table_insert, dim3((unsigned)((nH + 255) / 256)), dim3(256), 0, st,
+                           af->huniq.p, nH, af->tkeys.p, af->tvals.p, (uint32_t)(cap - 1),
+                           64 - log2cap);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
+
+        // --- pass 2a: FoundFragment counts per hash
+        af->counts.ensure((size_t)nH);
+        af->offsets.ensure((size_t)nH);
+        af->cursor.ensure((size_t)nH);
+        NPGX_HIP(hipMemsetAsync(af->counts.p, 0, (size_t)nH * 4, st));
+        NPGX_HIP(hipMemsetAsync(af->cursor.p, 0, (size_t)nH * 4, st));
+        ti = af->timer.begin("ff_count", st, n_windows * (0.375 + 12.0), n_windows);
+        hipLaunchKernelGGL(k_ff_count, grid, block, 0, st, A, T, af->counts.p);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
+        size_t b3 = 0;
+        NPGX_HIP(rocprim::exclusive_scan(nullptr, b3, af->counts.p, af->offsets.p, 0u, (size_t)nH,
+                                         rocprim::plus<uint32_t>(), st));
+        af->ensure_temp(b3);
+        ti = af->timer.begin("scan_cut", st, nH * 8.0, nH);
+        NPGX_HIP(rocprim::exclusive_scan(af->temp.p, b3, af->counts.p, af->offsets.p, 0u,
+                                         (size_t)nH, rocprim::plus<uint32_t>(), st));
+        af->cut.ensure(4);
+        hipLaunchKernelGGL(k_find_cut, dim3(1), dim3(64), 0, st, af->offsets.p, af->counts.p, nH,
+                           (uint64_t)af->opt.max_anchor_fragments, af->cut.p);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
+        NPGX_HIP(hipMemcpyAsync(hp, af->cut.p, 3 * 8, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipStreamSynchronize(st));
+        G = hp[0];
+        const uint64_t C = hp[1];
+        S.n_found_frags = (int64_t)hp[2];
+        S.n_kept_groups = (int64_t)G;
+        if (G > 0 && C > 0) {
+            const int idx_bits = bits_for(G);
+            NPGX_REQUIRE(idx_bits + key_bits <= 64, NPGX_ERR_RANGE,
+                         "FoundFragment sort key does not fit 64 bits");
+            af->cand.ensure(C);
+            af->cand_sorted.ensure(C);
+            ti = af->timer.begin("ff_scatter", st, n_windows * 0.375 + C * 24.0, n_windows);
+            hipLaunchKernelGGL(k_ff_scatter, grid, block, 0, st, A, T, af->huniq.p, G, af->offsets.p,
+                               af->cursor.p, key_bits, af->cand.p);
+            NPGX_HIP(hipGetLastError());
+            af->timer.end(ti, st);
+            size_t b4 = 0;
+            const unsigned end_bit = (unsigned)(idx_bits + key_bits);
+            NPGX_HIP(rocprim::radix_sort_keys(nullptr, b4, af->cand.p, af->cand_sorted.p, (size_t)C, 0u,
+                                              end_bit, st));
+            af->ensure_temp(b4);
+            ti = af->timer.begin("ff_sort", st, C * 32.0, (int64_t)C);
+            NPGX_HIP(rocprim::radix_sort_keys(af->temp.p, b4, af->cand.p, af->cand_sorted.p, (size_t)C,
+                                              0u, end_bit, st));
+            af->timer.end(ti, st);
+            const uint64_t keep = std::min<uint64_t>(C, (uint64_t)af->opt.max_anchor_fragments);
+            keys.resize(keep);
+            Hh.resize(G);
+            NPGX_HIP(hipMemcpyAsync(keys.data(), af->cand_sorted.p, keep * 8, hipMemcpyDeviceToHost, st));
+            NPGX_HIP(hipMemcpyAsync(Hh.data(), af->huniq.p, G * 8, hipMemcpyDeviceToHost, st));
+            NPGX_HIP(hipStreamSynchronize(st));
+        }
+    }
+
+    // --- fragmenttg_postprocess (AnchorFinder.cpp:356-391) on the truncated list
+    std::vector<uint64_t> prefix2(R);
+    for (int32_t r = 0; r < R; r++) prefix2[r] = 2ull * meta[r].order_off;
+    const uint64_t key_mask = key_bits >= 64 ? ~0ull : ((1ull << key_bits) - 1);
+    af->r_block_start.clear();
+    af->r_seq.clear();
+    af->r_min.clear();
+    af->r_max.clear();
+    af->r_ori.clear();
+    const bool sort_used = !af->used.empty();
+    size_t i = 0;
+    bool first_group = true;
+    while (i < keys.size()) {
+        const uint64_t idx = keys[i] >> key_bits;
+        size_t j = i + 1;
+        while (j < keys.size() && (keys[j] >> key_bits) == idx) j++;
+        if (!first_group) af->used.push_back(Hh[idx]);  // quirk: not the first group
+        first_group = false;
+        if (j - i >= 2) {
+            af->r_block_start.push_back((int64_t)af->r_seq.size());
+            for (size_t q = i; q < j; q++) {
+                const uint64_t key2 = keys[q] & key_mask;
+                const int32_t r = (int32_t)(std::upper_bound(prefix2.begin(), prefix2.end(), key2) -
+                                            prefix2.begin()) - 1;
+                const uint64_t pos2 = key2 - prefix2[r];
+                const uint64_t size = (uint64_t)meta[r].size;
+                const bool direct = pos2 < size;   // FoundFragment::make_fragment :240-246
+                const int64_t mn = (int64_t)(direct ? pos2 : pos2 - size);
+                af->r_seq.push_back(ss->by_rank[r]);
+                af->r_min.push_back(mn);
+                af->r_max.push_back(mn + k - 1);
+                af->r_ori.push_back(direct ? 1 : -1);
+            }
+        }
+        i = j;
+    }
+    af->r_block_start.push_back((int64_t)af->r_seq.size());
+    if (sort_used) std::sort(af->used.begin(), af->used.end());
+    if (af->used.size() != (size_t)S.n_used) af->used_dirty = true;
+    S.n_blocks = (int64_t)af->r_block_start.size() - 1;
+    S.n_fragments = (int64_t)af->r_seq.size();
+    S.n_used = (int64_t)af->used.size();
+    af->has_result = true;
+}
+
+}  // namespace npgx
+
+extern "C" {
+
+void npgx_af_default_options(npgx_af_options* o) {
+    if (!o) return;
+    memset(o, 0, sizeof(*o));
+    o->anchor_size = 20;            // ANCHOR_SIZE
+    o->anchor_similar = 1;
+    o->anchor_fp_x1e4 = 1000;       // ANCHOR_FP 0.1
+    o->max_anchor_fragments = 100000;  // MAX_ANCHOR_FRAGMENTS
+    o->bloom_seed = 1;
+}
+
+int npgx_af_create(const npgx_af_options* o, npgx_af** out) {
+    return guard([&] {
+        NPGX_REQUIRE(o && out, NPGX_ERR_ARG, "null argument");
+        // option rules (AnchorFinder.cpp:49-51)
+        NPGX_REQUIRE(o->anchor_size > 0, NPGX_ERR_ARG, "Option rule failed: anchor-size > 0");
+        NPGX_REQUIRE(o->anchor_size <= 32, NPGX_ERR_ARG, "Option rule failed: anchor-size <= 32");
+        NPGX_REQUIRE(o->anchor_fp_x1e4 > 0 && o->anchor_fp_x1e4 < 10000, NPGX_ERR_ARG,
+                     "anchor-fp must be in (0, 1)");
+        NPGX_REQUIRE(o->max_anchor_fragments >= 0, NPGX_ERR_ARG, "max-anchor-fragments < 0");
+        NPGX_REQUIRE(o->n_bloom_params >= 0 && o->n_bloom_params <= MAX_KB, NPGX_ERR_ARG,
+                     "n_bloom_params out of range");
+        int dev = current_device_checked();
+        auto* af = new npgx_af;
+        af->opt = *o;
+        af->opt.bloom_params = nullptr;
+        if (o->n_bloom_params > 0)
+            af->explicit_params.assign(o->bloom_params, o->bloom_params + o->n_bloom_params);
+        af->device = dev;
+        if (hipStreamCreateWithFlags(&af->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc((void**)&af->h_pinned, 64) != hipSuccess) {
+            delete af;
+            throw Error(NPGX_ERR_HIP, "stream / pinned allocation failed");
+        }
+        *out = af;
+    });
+}
+
+int npgx_af_run(npgx_af* af, const npgx_seqset* s) {
+    return guard([&] {
+        NPGX_REQUIRE(af && s, NPGX_ERR_ARG, "null argument");
+        af_run(af, s);
+    });
+}
+
+int npgx_af_stats_get(const npgx_af* af, npgx_af_stats* out) {
+    return guard([&] {
+        NPGX_REQUIRE(af && out, NPGX_ERR_ARG, "null argument");
+        *out = af->stats;
+    });
+}
+
+int npgx_af_result_counts(const npgx_af* af, int64_t* nb, int64_t* nf) {
+    return guard([&] {
+        NPGX_REQUIRE(af && nb && nf, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(af->has_result, NPGX_ERR_STATE, "no AnchorFinder result yet");
+        *nb = (int64_t)af->r_block_start.size() - 1;
+        *nf = (int64_t)af->r_seq.size();
+    });
+}
+
+int npgx_af_result_copy(const npgx_af* af, int64_t* block_start, int32_t* seq, int64_t* min_pos,
+                        int64_t* max_pos, int8_t* ori) {
+    return guard([&] {
+        NPGX_REQUIRE(af, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(af->has_result, NPGX_ERR_STATE, "no AnchorFinder result yet");
+        const size_t nf = af->r_seq.size();
+        if (block_start) memcpy(block_start, af->r_block_start.data(), af->r_block_start.size() * 8);
+        if (seq) memcpy(seq, af->r_seq.data(), nf * 4);
+        if (min_pos) memcpy(min_pos, af->r_min.data(), nf * 8);
+        if (max_pos) memcpy(max_pos, af->r_max.data(), nf * 8);
+        if (ori) memcpy(ori, af->r_ori.data(), nf);
+    });
+}
+
+int npgx_af_used_hashes(const npgx_af* af, uint64_t* out, int64_t cap, int64_t* n) {
+    return guard([&] {
+        NPGX_REQUIRE(af && n, NPGX_ERR_ARG, "null argument");
+        *n = (int64_t)af->used.size();
+        if (out) memcpy(out, af->used.data(), (size_t)std::min<int64_t>(cap, *n) * 8);
+    });
+}
+
+int npgx_af_clear_used(npgx_af* af) {
+    return guard([&] {
+        NPGX_REQUIRE(af, NPGX_ERR_ARG, "null argument");
+        af->used.clear();
+        af->used_dirty = true;
+    });
+}
+
+int npgx_af_kernel_times(const npgx_af* af, npgx_kernel_time* out, int32_t cap, int32_t* n) {
+    return guard([&] {
+        NPGX_REQUIRE(af && n && (out || cap == 0), NPGX_ERR_ARG, "null argument");
+        af->timer.copy_out(out, cap, n);
+    });
+}
+
+void npgx_af_free(npgx_af* af) {
+    if (!af) return;
+    (void)hipSetDevice(af->device);
+    if (af->stream) (void)hipStreamDestroy(af->stream);
+    if (af->h_pinned) (void)hipHostFree(af->h_pinned);
+    delete af;
+}
+
+}  // extern "C"

@@ -1,0 +1,148 @@
+// common.hpp -- error plumbing, device buffers and small device helpers shared by
+// the npge_amd HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/npge_amd.h"
+
+namespace npgx {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& msg);
+
+#define NPGX_HIP(call)                                                                \
+    do {                                                                              \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            throw ::npgx::Error(NPGX_ERR_HIP, std::string(#call) + ": " +             \
+                                                  hipGetErrorString(e_));             \
+    } while (0)
+
+#define NPGX_REQUIRE(cond, code, msg)                     \
+    do {                                                  \
+        if (!(cond)) throw ::npgx::Error((code), (msg));  \
+    } while (0)
+
+// Runs f, converts exceptions into a status code + thread-local message.
+template <class F>
+int guard(F&& f) {
+    try {
+        f();
+        return NPGX_OK;
+    } catch (const Error& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return NPGX_ERR_ARG;
+    } catch (...) {
+        set_last_error("unknown error");
+        return NPGX_ERR_ARG;
+    }
+}
+
+// Growable device buffer (capacity kept across runs so repeated steps do not
+// re-allocate).
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    T* ensure(size_t n) {
+        if (n == 0) n = 1;
+        if (n > cap) {
+            release();
+            NPGX_HIP(hipMalloc(&p, n * sizeof(T)));
+            cap = n;
+        }
+        return p;
+    }
+};
+
+// Stage timer: pairs of HIP events on one stream.
+struct StageTimer {
+    struct Rec {
+        std::string name;
+        hipEvent_t a, b;
+        double bytes;
+        int64_t units;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    ~StageTimer() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            NPGX_HIP(hipEventCreate(&e));
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void reset() {
+        recs.clear();
+        used = 0;
+    }
+    size_t begin(const char* name, hipStream_t s, double bytes, int64_t units) {
+        Rec r{name, get(), get(), bytes, units};
+        NPGX_HIP(hipEventRecord(r.a, s));
+        recs.push_back(r);
+        return recs.size() - 1;
+    }
+    void end(size_t i, hipStream_t s) { NPGX_HIP(hipEventRecord(recs[i].b, s)); }
+    int copy_out(npgx_kernel_time* out, int32_t cap, int32_t* n) const {
+        int32_t k = 0;
+        for (const Rec& r : recs) {
+            if (k >= cap) break;
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = -1.f;
+            snprintf(out[k].name, sizeof(out[k].name), "%s", r.name.c_str());
+            out[k].ms = ms;
+            out[k].bytes = r.bytes;
+            out[k].units = r.units;
+            k++;
+        }
+        *n = (int32_t)recs.size();
+        return NPGX_OK;
+    }
+};
+
+int current_device_checked();
+
+}  // namespace npgx
+
+// ----------------------------------------------------------------- sequence set
+struct npgx_seqset {
+    int device = 0;
+    int32_t n = 0;
+    std::vector<std::string> names;
+    std::vector<std::string> data;       // after to_atgcn (input order)
+    std::vector<int32_t> rank_of;        // input index -> rank
+    std::vector<int32_t> by_rank;        // rank -> input index
+    // device layout, in rank order
+    std::vector<int64_t> word_off;       // first uint64 word of rank r (32 bases/word)
+    std::vector<int64_t> n_off;          // first uint64 word of the N bitmap of rank r
+    int64_t total_words = 0, total_nwords = 0;
+    npgx::DevBuf<uint64_t> words, nmask;
+};

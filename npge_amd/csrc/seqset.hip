@@ -1,0 +1,251 @@
+// seqset.hip -- device-resident 2-bit sequence storage.
+//
+// Replaces the CompactLowNSequence storage (src/model/Sequence.cpp:525-600: 4 nt
+// per byte, A0 T1 G2 C3, LSB first, plus a sorted vector of N positions) with an
+// HBM layout built for coalesced window loads:
+//   * words: uint64, 32 bases per word, base i of a sequence at bits 2*(i%32) of
+//     word off+i/32 -- byte-for-byte the reference's packing, widened to 64 bits;
+//     every sequence starts on a word boundary and is followed by one zero word so
+//     a window load may always read word w+1.
+//   * nmask: uint64, bit i%64 of word noff+i/64 set iff base i is N (N's 2-bit code
+//     is 0, as in CompactLowNSequence::set_item :587-591).
+// Sequences are stored in processing (rank) order: size desc, name asc, input
+// index asc (the pinned form of SeqI.hpp:54).
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+
+#include "common.hpp"
+
+namespace npgx {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+int current_device_checked() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        throw Error(NPGX_ERR_NODEV, "no HIP device available");
+    int d = 0;
+    NPGX_HIP(hipGetDevice(&d));
+    return d;
+}
+
+// Sequence::to_atgcn (Sequence.cpp:151-179) as a 256-entry table:
+// 0 = drop, else the output letter.
+static const unsigned char* atgcn_table() {
+    static unsigned char t[256];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        memset(t, 0, sizeof(t));
+        const char* keep = "ATGCN";
+        for (const char* c = keep; *c; c++) {
+            t[(unsigned char)*c] = (unsigned char)*c;
+            t[(unsigned char)tolower(*c)] = (unsigned char)*c;
+        }
+        const char* iupac = "RYMKWSBVHD";
+        for (const char* c = iupac; *c; c++) {
+            t[(unsigned char)*c] = 'N';
+            t[(unsigned char)tolower(*c)] = 'N';
+        }
+    });
+    return t;
+}
+
+std::string to_atgcn(const char* s, int64_t len) {
+    const unsigned char* t = atgcn_table();
+    std::string out;
+    out.resize((size_t)len);
+    int64_t k = 0;
+    for (int64_t i = 0; i < len; i++) {
+        unsigned char c = t[(unsigned char)s[i]];
+        if (c) out[(size_t)k++] = (char)c;
+    }
+    out.resize((size_t)k);
+    return out;
+}
+
+// One thread packs 32 bases of ASCII (already ATGCN) into one word; one wave's
+// 64 words also yield 32 N-bitmap words via pairs of lanes.
+__global__ void k_pack(const unsigned char* __restrict__ ascii, const int64_t* __restrict__ seq_word_off,
+                       const int64_t* __restrict__ seq_ascii_off, const int64_t* __restrict__ seq_n_off,
+                       const int64_t* __restrict__ seq_size, const int32_t* __restrict__ word_seq,
+                       int64_t total_words, uint64_t* __restrict__ words, uint64_t* __restrict__ nmask) {
+    int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= total_words) return;
+    int32_t r = word_seq[w];
+    int64_t local = w - seq_word_off[r];           // word index within the sequence
+    int64_t base0 = local * 32;
+    int64_t size = seq_size[r];
+    const unsigned char* src = ascii + seq_ascii_off[r] + base0;
+    uint64_t v = 0;
+    uint32_t nbits = 0;
+#pragma unroll 8
+    for (int j = 0; j < 32; j++) {
+        unsigned char c = (base0 + j < size) ? src[j] : 'A';
+        uint64_t code = (c == 'T') ? 1 : (c == 'G') ? 2 : (c == 'C') ? 3 : 0;
+        v |= code << (2 * j);
+        nbits |= (uint32_t)(c == 'N') << j;
+    }
+    words[w] = v;  // the trailing pad word of each sequence packs to 0
+    // N bitmap: word local/2 of the sequence gets bits from two packed words
+    int64_t nw = seq_n_off[r] + local / 2;
+    if (local % 2 == 0) {
+        // lower half written by the even word; the odd word ORs its half in.
+        atomicOr((unsigned long long*)&nmask[nw], (unsigned long long)nbits);
+    } else {
+        atomicOr((unsigned long long*)&nmask[nw], (unsigned long long)nbits << 32);
+    }
+}
+
+}  // namespace npgx
+
+using namespace npgx;
+
+extern "C" {
+
+const char* npgx_last_error(void) { return g_last_error.c_str(); }
+const char* npgx_version(void) { return "npge_amd 0.1 (gfx950)"; }
+
+int npgx_device_count(int32_t* n) {
+    return guard([&] {
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+        *n = c;
+    });
+}
+
+int npgx_set_device(int32_t device) {
+    return guard([&] { NPGX_HIP(hipSetDevice(device)); });
+}
+
+int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char* const* names,
+                       int32_t n, npgx_seqset** out) {
+    return guard([&] {
+        NPGX_REQUIRE(out && n >= 0 && (n == 0 || (seqs && lens)), NPGX_ERR_ARG,
+                     "npgx_seqset_create: bad arguments");
+        int dev = current_device_checked();
+        auto* s = new npgx_seqset;
+        try {
+            s->device = dev;
+            s->n = n;
+            s->names.resize(n);
+            s->data.resize(n);
+            for (int32_t i = 0; i < n; i++) {
+                NPGX_REQUIRE(lens[i] >= 0, NPGX_ERR_ARG, "negative sequence length");
+                s->names[i] = names && names[i] ? names[i] : "";
+                s->data[i] = to_atgcn(seqs[i], lens[i]);
+            }
+            // rank: size desc, name asc, input index asc
+            s->by_rank.resize(n);
+            std::iota(s->by_rank.begin(), s->by_rank.end(), 0);
+            std::sort(s->by_rank.begin(), s->by_rank.end(), [&](int32_t a, int32_t b) {
+                if (s->data[a].size() != s->data[b].size())
+                    return s->data[a].size() > s->data[b].size();
+                if (s->names[a] != s->names[b]) return s->names[a] < s->names[b];
+                return a < b;
+            });
+            s->rank_of.assign(n, 0);
+            for (int32_t r = 0; r < n; r++) s->rank_of[s->by_rank[r]] = r;
+            // layout
+            s->word_off.resize(n);
+            s->n_off.resize(n);
+            std::vector<int64_t> ascii_off(n), size_r(n);
+            std::vector<int32_t> word_seq;
+            int64_t wo = 0, no = 0, ao = 0;
+            for (int32_t r = 0; r < n; r++) {
+                int64_t sz = (int64_t)s->data[s->by_rank[r]].size();
+                int64_t nw = (sz + 31) / 32 + 1;           // + zero pad word
+                if (nw % 2) nw += 1;                       // keep N-word pairing aligned
+                s->word_off[r] = wo;
+                s->n_off[r] = no;
+                ascii_off[r] = ao;
+                size_r[r] = sz;
+                wo += nw;
+                no += nw / 2;
+                ao += sz;
+                word_seq.insert(word_seq.end(), (size_t)nw, r);
+            }
+            s->total_words = wo;
+            s->total_nwords = no;
+            s->words.ensure((size_t)wo);
+            s->nmask.ensure((size_t)no);
+            if (wo > 0) {
+                std::string ascii;
+                ascii.reserve((size_t)ao);
+                for (int32_t r = 0; r < n; r++) ascii += s->data[s->by_rank[r]];
+                DevBuf<unsigned char> d_ascii;
+                DevBuf<int64_t> d_wo, d_ao, d_no, d_sz;
+                DevBuf<int32_t> d_ws;
+                d_ascii.ensure(ascii.size());
+                d_wo.ensure(n);
+                d_ao.ensure(n);
+                d_no.ensure(n);
+                d_sz.ensure(n);
+                d_ws.ensure(word_seq.size());
+                NPGX_HIP(hipMemcpy(d_ascii.p, ascii.data(), ascii.size(), hipMemcpyHostToDevice));
+                NPGX_HIP(hipMemcpy(d_wo.p, s->word_off.data(), n * 8, hipMemcpyHostToDevice));
+                NPGX_HIP(hipMemcpy(d_ao.p, ascii_off.data(), n * 8, hipMemcpyHostToDevice));
+                NPGX_HIP(hipMemcpy(d_no.p, s->n_off.data(), n * 8, hipMemcpyHostToDevice));
+                NPGX_HIP(hipMemcpy(d_sz.p, size_r.data(), n * 8, hipMemcpyHostToDevice));
+                NPGX_HIP(hipMemcpy(d_ws.p, word_seq.data(), word_seq.size() * 4,
+                                   hipMemcpyHostToDevice));
+                NPGX_HIP(hipMemset(s->nmask.p, 0, (size_t)no * 8));
+                int threads = 256;
+                int64_t blocks = (wo + threads - 1) / threads;
+                hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(threads), 0, 0, d_ascii.p,
+                                   d_wo.p, d_ao.p, d_no.p, d_sz.p, d_ws.p, wo, s->words.p,
+                                   s->nmask.p);
+                NPGX_HIP(hipGetLastError());
+                NPGX_HIP(hipDeviceSynchronize());
+            }
+            *out = s;
+        } catch (...) {
+            delete s;
+            throw;
+        }
+    });
+}
+
+int npgx_seqset_count(const npgx_seqset* s, int32_t* n) {
+    return guard([&] {
+        NPGX_REQUIRE(s && n, NPGX_ERR_ARG, "null argument");
+        *n = s->n;
+    });
+}
+
+int npgx_seqset_size(const npgx_seqset* s, int32_t index, int64_t* size) {
+    return guard([&] {
+        NPGX_REQUIRE(s && size && index >= 0 && index < s->n, NPGX_ERR_ARG, "bad index");
+        *size = (int64_t)s->data[index].size();
+    });
+}
+
+int npgx_seqset_rank(const npgx_seqset* s, int32_t index, int32_t* rank) {
+    return guard([&] {
+        NPGX_REQUIRE(s && rank && index >= 0 && index < s->n, NPGX_ERR_ARG, "bad index");
+        *rank = s->rank_of[index];
+    });
+}
+
+int npgx_seqset_text(const npgx_seqset* s, int32_t index, int64_t start, int64_t len, char* out) {
+    return guard([&] {
+        NPGX_REQUIRE(s && out && index >= 0 && index < s->n, NPGX_ERR_ARG, "bad index");
+        const std::string& d = s->data[index];
+        NPGX_REQUIRE(start >= 0 && len >= 0 && start + len <= (int64_t)d.size(), NPGX_ERR_RANGE,
+                     "range outside sequence");
+        memcpy(out, d.data() + start, (size_t)len);
+    });
+}
+
+int npgx_seqset_device_bytes(const npgx_seqset* s, int64_t* bytes) {
+    return guard([&] {
+        NPGX_REQUIRE(s && bytes, NPGX_ERR_ARG, "null argument");
+        *bytes = (s->total_words + s->total_nwords) * 8;
+    });
+}
+
+void npgx_seqset_free(npgx_seqset* s) { delete s; }
+
+}  // extern "C"

@@ -12,7 +12,8 @@ import pytest
 
 from oracle import oracle as orc
 from npge_amd import io as nio
-from npge_amd.model import Block, Fragment, Sequence, blockset_hash, normalized_blocks
+from npge_amd.model import Sequence, blockset_hash, normalized_blocks
+from helpers import af_blocks_from_result
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -144,16 +145,6 @@ def _load_case(case):
     with open(os.path.join(d, "out.fasta")) as f:
         exp = nio.read_blockset(f.read())
     return recs, exp
-
-
-def af_blocks_from_result(r, seqs):
-    blocks = []
-    bs = r["block_start"]
-    for b in range(len(bs) - 1):
-        frs = [Fragment(seqs[int(r["seq"][i])], int(r["min_pos"][i]), int(r["max_pos"][i]),
-                        int(r["ori"][i])) for i in range(bs[b], bs[b + 1])]
-        blocks.append(Block(frs))
-    return blocks
 
 
 @pytest.mark.parametrize("case", ["1", "bug-n-in-init-frame", "complement-no-inverse",

@@ -1,0 +1,718 @@
+// similar_aligner.hip -- batched AbstractAligner::align_seqs with aligner-type
+// "similar" (SimilarAligner::similar_aligner, src/algo/SimilarAligner.cpp:487-501)
+// or "dummy" (DummyAligner.cpp:18-26) on MI355X.
+//
+// Blocks are independent ("Blocks should not interfere", BlocksJobs.hpp:49-53),
+// so a batch of alignment problems (one per block) is the batch axis: a
+// persistent grid of single-wave workgroups pulls jobs from an atomic counter
+// (heaviest first).  Inside a job, lanes are rows.  Phases per job:
+//   1. process_seqs on the input rows           -> A   (sa_device.hpp)
+//   2. fix_bad_regions (:428-459) A -> B: column-parallel good-column scan,
+//      FindLowSimilar::make_regions/reduce_regions (FindLowSimilar.cpp:62-130),
+//      re-alignment of every bad region (gap-filtered, reversed) kept only if
+//      its identical-column score grows
+//   3. realing_end (:461-484) on B
+//   4. AbstractAligner::remove_gaps (AbstractAligner.cpp:89-102)
+// Empty rows are removed before and re-added as all-gap rows after
+// (AbstractAligner.cpp:104-143).  Output columns are bounded by the sum of the
+// row lengths (every column holds a letter); a job first gets a tighter
+// capacity and is re-run at the full bound if it overflows.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <string>
+
+#include "common.hpp"
+#include "sa_device.hpp"
+
+namespace npgx {
+
+using namespace sa;
+
+struct SaJob {
+    int64_t row0;       // first non-empty row (index into row_off / row_len)
+    int64_t scratch;    // byte offset of this job's A|B|C scratch
+    int32_t n;          // non-empty rows (<= 64)
+    int32_t cap;        // column capacity of A, B and C rows
+};
+
+struct SaArgs {
+    const char* rows;
+    const int64_t* row_off;
+    const int32_t* row_len;
+    const SaJob* jobs;
+    const int32_t* order;      // job processing order (heaviest first)
+    int32_t n_jobs;
+    int32_t aligner_type;      // 0 similar, 1 dummy
+    unsigned char* scratch;
+    int32_t* job_len;
+    int32_t* job_status;       // 0 ok, 1 capacity overflow
+    unsigned int* next_job;
+    // per-slot scratch
+    unsigned long long* tkeys;
+    unsigned long long* tmask;
+    uint32_t tcap_log2;
+    uint32_t* slot_epoch;
+    const char** st_p;
+    int* st_len;
+    int* st_pos;
+    int* st_col;
+    int32_t st_depth_max;
+    int4* regions;
+    unsigned char* good_col;
+    int32_t slot_cols;         // regions / good_col entries per slot
+    Params P;
+};
+
+// number of columns c in [c0, c1) identical over all rows (score_of :416-426)
+__device__ int count_equal_cols(const WaveCtx& w, const char* buf, int cap, int c0, int c1,
+                                unsigned char* flags) {
+    int cnt = 0;
+    for (int c = c0 + w.lane; c < c1; c += 64) {
+        const char x = buf[c];
+        bool eq = true;
+        for (int r = 1; r < w.n; r++) eq &= (buf[(size_t)r * cap + c] == x);
+        cnt += eq;
+        if (flags) flags[c] = eq;
+    }
+    return wave_sum(cnt);
+}
+
+__device__ void copy_cols(const WaveCtx& w, const char* src, char* dst, int cap, int s0, int d0,
+                          int len) {
+    if (!w.act) return;
+    const char* a = src + (size_t)w.lane * cap + s0;
+    char* b = dst + (size_t)w.lane * cap + d0;
+    for (int j = 0; j < len; j++) b[j] = a[j];
+}
+
+// gap-filtered, reversed copy of row segment [s0, s1) into C row (view returned)
+__device__ View filter_reverse(const WaveCtx& w, const char* src, char* C, int cap, int s0, int s1) {
+    View v{C + (size_t)w.lane * cap, 0, 1};
+    if (!w.act) return v;
+    const char* a = src + (size_t)w.lane * cap;
+    char* c = C + (size_t)w.lane * cap;
+    int k = 0;
+    for (int j = s1 - 1; j >= s0; j--)
+        if (a[j] != '-') c[k++] = a[j];
+    v.len = k;
+    return v;
+}
+
+// FindLowSimilar::make_regions (:62-80) from good_col[0..L)
+__device__ int make_regions(const WaveCtx& w, const unsigned char* good, int L, int wf, int4* reg) {
+    int R = 0;
+    for (int base = 0; base < L; base += 64) {
+        const int j = base + w.lane;
+        const bool in = j < L;
+        const int g = in ? good[j] : 0;
+        const int gp = (in && j > 0) ? good[j - 1] : -1;
+        const bool b = in && (j == 0 || g != gp);
+        const unsigned long long bm = ballot(b);
+        const int idx = R + __popcll(bm & ((1ull << w.lane) - 1ull));
+        if (b) reg[idx] = make_int4(j, 0, g, 0);
+        R += __popcll(bm);
+    }
+    __syncthreads();
+    for (int i = w.lane; i < R; i += 64) {
+        int4 r = reg[i];
+        const int stop = (i + 1 < R) ? reg[i + 1].x - 1 : L - 1;
+        const int len = stop - r.x + 1;
+        r.y = stop;
+        r.w = r.z ? len : len * wf;  // Region::set_weight :48-54
+        reg[i] = r;
+    }
+    __syncthreads();
+    return R;
+}
+
+// FindLowSimilar::reduce_regions (:121-130) with find_min_region (:82-92) and
+// merge_region (:94-119)
+__device__ int reduce_regions(const WaveCtx& w, int4* reg, int R, int min_length) {
+    while (R >= 2) {
+        int bw = 0x7fffffff, bi = 0x7fffffff;
+        for (int i = w.lane; i < R; i += 64) {
+            const int wt = reg[i].w;
+            if (wt < bw) {
+                bw = wt;
+                bi = i;
+            }
+        }
+        // first index of the minimum weight
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int ow = __shfl_xor(bw, o), oi = __shfl_xor(bi, o);
+            if (ow < bw || (ow == bw && oi < bi)) {
+                bw = ow;
+                bi = oi;
+            }
+        }
+        if (bw >= min_length) break;
+        const int mi = bi;
+        int4 nr = reg[mi];
+        const int good = nr.z;
+        int first = mi, last = mi;
+        if (mi > 0) {
+            const int4 p = reg[mi - 1];
+            nr.x = p.x;
+            nr.w += p.w;
+            first = mi - 1;
+        }
+        if (mi < R - 1) {
+            const int4 q = reg[mi + 1];
+            nr.y = q.y;
+            nr.w += q.w;
+            last = mi + 1;
+        }
+        nr.z = good == 0 ? 1 : 0;
+        __syncthreads();
+        if (w.lane == 0) reg[first] = nr;
+        const int shiftn = last - first;
+        if (shiftn > 0) {
+            for (int base = last + 1; base < R; base += 64) {
+                const int i = base + w.lane;
+                int4 x;
+                if (i < R) x = reg[i];
+                __syncthreads();
+                if (i < R) reg[i - shiftn] = x;
+                __syncthreads();
+            }
+        }
+        R -= shiftn;
+        __syncthreads();
+    }
+    return R;
+}
+
+// AbstractAligner.cpp:89-102: drop columns that are '-' in every row
+__device__ int remove_pure_gap_cols(const WaveCtx& w, char* buf, int cap, int L) {
+    int dest = 0;
+    for (int base = 0; base < L; base += 64) {
+        const int c = base + w.lane;
+        bool keep = false;
+        if (c < L)
+            for (int r = 0; r < w.n && !keep; r++) keep = buf[(size_t)r * cap + c] != '-';
+        const unsigned long long km = ballot(keep);
+        if (km == ((base + 64 <= L) ? ~0ull : ((1ull << (L - base)) - 1ull)) && dest == base) {
+            dest += __popcll(km);  // nothing removed so far
+            continue;
+        }
+        __syncthreads();
+        // move kept columns of this chunk left (row by row, lanes = columns)
+        const int to = dest + __popcll(km & ((1ull << w.lane) - 1ull));
+        for (int r = 0; r < w.n; r++) {
+            char x = 0;
+            if (keep) x = buf[(size_t)r * cap + c];
+            __syncthreads();
+            if (keep) buf[(size_t)r * cap + to] = x;
+            __syncthreads();
+        }
+        dest += __popcll(km);
+    }
+    return dest;
+}
+
+__global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
+    const int lane = threadIdx.x;
+    Slot S;
+    const size_t slot = blockIdx.x;
+    const size_t tcap = (size_t)1 << a.tcap_log2;
+    S.tkeys = a.tkeys + slot * tcap;
+    S.tmask = a.tmask + slot * tcap;
+    S.tcap_log2 = a.tcap_log2;
+    S.epoch = a.slot_epoch[slot];
+    const size_t stn = (size_t)a.st_depth_max * 64;
+    S.st_p = a.st_p + slot * stn;
+    S.st_len = a.st_len + slot * stn;
+    S.st_pos = a.st_pos + slot * stn;
+    S.st_col = a.st_col + slot * a.st_depth_max;
+    S.st_depth_max = a.st_depth_max;
+    S.regions = a.regions + slot * (size_t)a.slot_cols;
+    S.good_col = a.good_col + slot * (size_t)a.slot_cols;
+
+    while (true) {
+        unsigned int jn = 0;
+        if (lane == 0) jn = atomicAdd(a.next_job, 1u);
+        jn = __shfl(jn, 0);
+        if (jn >= (unsigned)a.n_jobs) break;
+        const int j = a.order[jn];
+        const SaJob job = a.jobs[j];
+        const int n = job.n;
+        if (n == 0) {
+            if (lane == 0) {
+                a.job_len[j] = 0;
+                a.job_status[j] = 0;
+            }
+            continue;
+        }
+        WaveCtx w;
+        w.lane = lane;
+        w.n = n;
+        w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+        w.act = lane < n;
+        const int cap = job.cap;
+        char* A = (char*)(a.scratch + job.scratch);
+        char* B = A + (size_t)n * cap;
+        char* C = B + (size_t)n * cap;
+        View v0{nullptr, 0, 1};
+        if (w.act) {
+            v0.p = a.rows + a.row_off[job.row0 + lane];
+            v0.len = a.row_len[job.row0 + lane];
+        }
+        bool ovf = false;
+        int L = 0;
+        if (a.aligner_type == 1) {
+            // DummyAligner: pad to the longest row
+            const int m = wave_max(v0.len);
+            if (m > cap) ovf = true;
+            else if (w.act) {
+                char* b = B + (size_t)lane * cap;
+                for (int q = 0; q < v0.len; q++) b[q] = v0.p[q];
+                for (int q = v0.len; q < m; q++) b[q] = '-';
+            }
+            L = m;
+        } else {
+            // 1. process_seqs
+            Proc pr(w, a.P, S, Out{A, cap});
+            const int L0 = pr.run(v0, 0);
+            ovf = any_lane(w, pr.ovf);
+            __syncthreads();
+            if (!ovf) {
+                // 2. fix_bad_regions
+                count_equal_cols(w, A, cap, 0, L0, S.good_col);
+                __syncthreads();
+                int R = make_regions(w, S.good_col, L0, a.P.wf, S.regions);
+                R = reduce_regions(w, S.regions, R, a.P.min_length);
+                int colB = 0;
+                Proc q(w, a.P, S, Out{B, cap});
+                for (int ri = 0; ri < R && !ovf; ri++) {
+                    const int4 rg = S.regions[ri];
+                    const int len = rg.y - rg.x + 1;
+                    if (colB + len > cap) {
+                        ovf = true;
+                        break;
+                    }
+                    if (rg.z) {
+                        copy_cols(w, A, B, cap, rg.x, colB, len);
+                        colB += len;
+                        continue;
+                    }
+                    int before = 0;
+                    for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
+                    before = wave_sum(before);
+                    const View cv = filter_reverse(w, A, C, cap, rg.x, rg.y + 1);
+                    const int Lc = q.run(cv, colB);
+                    if (any_lane(w, q.ovf)) {
+                        ovf = true;
+                        break;
+                    }
+                    __syncthreads();
+                    const int after = count_equal_cols(w, B, cap, colB, colB + Lc, nullptr);
+                    __syncthreads();
+                    if (after > before) {
+                        q.reverse_cols(colB, colB + Lc);
+                        colB += Lc;
+                    } else {
+                        copy_cols(w, A, B, cap, rg.x, colB, len);
+                        colB += len;
+                    }
+                    __syncthreads();
+                }
+                // 3. realing_end
+                L = colB;
+                if (!ovf && L >= 2) {
+                    int prefix = L - a.P.ac;
+                    if (prefix < 1) prefix = 1;
+                    const View tv = filter_reverse(w, B, C, cap, prefix, L);
+                    Proc t(w, a.P, S, Out{B, cap});
+                    const int Lt = t.run(tv, prefix);
+                    if (any_lane(w, t.ovf)) ovf = true;
+                    else {
+                        t.reverse_cols(prefix, prefix + Lt);
+                        L = prefix + Lt;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // 4. remove pure-gap columns
+        if (!ovf) L = remove_pure_gap_cols(w, B, cap, L);
+        if (lane == 0) {
+            a.job_len[j] = ovf ? 0 : L;
+            a.job_status[j] = ovf ? 1 : 0;
+        }
+        __syncthreads();
+    }
+    if (lane == 0) a.slot_epoch[slot] = S.epoch;
+}
+
+struct GatherRow {
+    int64_t out_off;    // output byte offset
+    int64_t src;        // scratch byte offset of the aligned row (-1: empty row)
+    int32_t len;        // job alignment length
+    int32_t pad;
+};
+
+__global__ void k_gather_rows(const GatherRow* rows, int64_t n, const unsigned char* scratch, char* out) {
+    const int64_t r = blockIdx.x;
+    if (r >= n) return;
+    const GatherRow g = rows[r];
+    char* d = out + g.out_off;
+    if (g.src < 0) {
+        for (int c = threadIdx.x; c < g.len; c += blockDim.x) d[c] = '-';
+    } else {
+        const char* s = (const char*)scratch + g.src;
+        for (int c = threadIdx.x; c < g.len; c += blockDim.x) d[c] = s[c];
+    }
+}
+
+int weight_factor(int64_t min_identity_x1e4) {
+    // FindLowSimilar::get_weight_factor with Decimal arithmetic (Decimal.hpp)
+    int64_t mi = std::min<int64_t>(min_identity_x1e4, 9900);
+    const int64_t one = 10000;
+    const int64_t q = one * 10000 / (one - mi);          // Decimal division
+    const int64_t ip = q / 10000, fr = q % 10000;       // q > 0
+    return (int)(fr < 5000 ? ip : ip + 1);               // Decimal::round
+}
+
+}  // namespace npgx
+
+using namespace npgx;
+
+struct npgx_aligner {
+    npgx_align_options opt;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf<char> d_rows;
+    DevBuf<int64_t> d_row_off;
+    DevBuf<int32_t> d_row_len;
+    DevBuf<SaJob> d_jobs;
+    DevBuf<int32_t> d_order, d_job_len, d_job_status;
+    DevBuf<unsigned int> d_next;
+    DevBuf<unsigned char> d_scratch;
+    DevBuf<unsigned long long> tkeys, tmask;
+    DevBuf<uint32_t> slot_epoch;
+    size_t slots_alloc = 0, tcap_alloc = 0, tcap_cur = 0;
+    DevBuf<const char*> st_p;
+    DevBuf<int> st_len, st_pos, st_col;
+    DevBuf<int4> regions;
+    DevBuf<unsigned char> good_col;
+    DevBuf<GatherRow> d_gather;
+    DevBuf<char> d_out;
+    // last result
+    std::vector<char> out;
+    std::vector<int64_t> out_off;
+    std::vector<int64_t> job_len;
+    bool has_result = false;
+    StageTimer timer;
+};
+
+namespace npgx {
+
+static void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
+                        const int32_t* job_row_start, int32_t n_jobs) {
+    NPGX_HIP(hipSetDevice(al->device));
+    hipStream_t st = al->stream;
+    al->timer.reset();
+    al->has_result = false;
+    const npgx_align_options& o = al->opt;
+    NPGX_REQUIRE(n_jobs >= 0, NPGX_ERR_ARG, "n_jobs < 0");
+    const int64_t n_rows = n_jobs ? (int64_t)job_row_start[n_jobs] - job_row_start[0] : 0;
+    // non-empty rows, packed
+    std::vector<SaJob> jobs(n_jobs);
+    std::vector<int64_t> ne_off;
+    std::vector<int32_t> ne_len;
+    std::vector<int64_t> row_ne(n_rows > 0 ? n_rows : 1, -1);  // row -> index of non-empty row
+    std::vector<double> cost(n_jobs);
+    int64_t scratch = 0;
+    int max_n = 1, max_len = 1, max_cap = 1;
+    const int64_t r_base = n_jobs ? job_row_start[0] : 0;
+    for (int32_t j = 0; j < n_jobs; j++) {
+        const int64_t r0 = job_row_start[j], r1 = job_row_start[j + 1];
+        NPGX_REQUIRE(r1 >= r0, NPGX_ERR_ARG, "job_row_start not monotone");
+        SaJob& J = jobs[j];
+        J.row0 = (int64_t)ne_len.size();
+        int n = 0;
+        int64_t sum = 0;
+        int mx = 0;
+        for (int64_t r = r0; r < r1; r++) {
+            const int64_t len = row_off[r + 1] - row_off[r];
+            NPGX_REQUIRE(len >= 0 && len < (1ll << 30), NPGX_ERR_RANGE, "row length out of range");
+            if (len == 0) continue;
+            if (o.aligner_type == 0) {
+                for (int64_t q = 0; q < len; q++) {
+                    const char c = rows[row_off[r] + q];
+                    NPGX_REQUIRE(c == 'A' || c == 'C' || c == 'G' || c == 'T' || c == 'N', NPGX_ERR_ARG,
+                                 "similar aligner rows must be upper-case ATGCN");
+                }
+            }
+            row_ne[r - r_base] = (int64_t)ne_len.size();
+            ne_off.push_back(row_off[r]);
+            ne_len.push_back((int32_t)len);
+            n++;
+            sum += len;
+            mx = std::max<int>(mx, (int)len);
+        }
+        NPGX_REQUIRE(n <= 64, NPGX_ERR_RANGE, "more than 64 non-empty rows in one alignment");
+        J.n = n;
+        // first attempt: 2*max+64 columns (the full bound is the sum of lengths)
+        int64_t cap = std::min<int64_t>(sum, 2ll * mx + 64);
+        if (o.aligner_type == 1) cap = mx;
+        J.cap = (int32_t)std::max<int64_t>(cap, 1);
+        J.scratch = scratch;
+        scratch += (3ll * n * J.cap + 255) & ~255ll;
+        cost[j] = double(n) * double(sum);
+        max_n = std::max(max_n, n);
+        max_len = std::max(max_len, mx);
+        max_cap = std::max<int>(max_cap, J.cap);
+    }
+    std::vector<int32_t> order(n_jobs);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+
+    // device upload of rows (only the non-empty ones, compacted)
+    int64_t bytes = 0;
+    for (size_t i = 0; i < ne_len.size(); i++) bytes += ne_len[i];
+    std::vector<char> packed((size_t)std::max<int64_t>(bytes, 1));
+    std::vector<int64_t> poff(ne_len.size());
+    int64_t b = 0;
+    for (size_t i = 0; i < ne_len.size(); i++) {
+        poff[i] = b;
+        memcpy(packed.data() + b, rows + ne_off[i], (size_t)ne_len[i]);
+        b += ne_len[i];
+    }
+    al->d_rows.ensure(packed.size());
+    al->d_row_off.ensure(poff.size());
+    al->d_row_len.ensure(ne_len.size());
+    al->d_jobs.ensure(jobs.size());
+    al->d_order.ensure(order.size());
+    al->d_job_len.ensure(jobs.size());
+    al->d_job_status.ensure(jobs.size());
+    al->d_next.ensure(1);
+    NPGX_HIP(hipMemcpyAsync(al->d_rows.p, packed.data(), packed.size(), hipMemcpyHostToDevice, st));
+    if (!poff.empty()) {
+        NPGX_HIP(hipMemcpyAsync(al->d_row_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, st));
+        NPGX_HIP(hipMemcpyAsync(al->d_row_len.p, ne_len.data(), ne_len.size() * 4, hipMemcpyHostToDevice, st));
+    }
+    int wf = weight_factor(o.min_identity_x1e4);
+    Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
+
+    std::vector<int32_t> jlen(n_jobs), jstat(n_jobs);
+    std::vector<std::string> row_out((size_t)std::max<int64_t>(n_rows, 0));
+    al->job_len.assign(n_jobs, 0);
+    std::vector<int32_t> todo = order;
+    for (int attempt = 0; attempt < 2 && !todo.empty(); attempt++) {
+        if (attempt == 1) {  // re-run overflowed jobs at the proven bound (sum of lengths)
+            scratch = 0;
+            max_cap = 1;
+            for (int32_t j : todo) {
+                SaJob& J = jobs[j];
+                int64_t sum = 0;
+                for (int i = 0; i < J.n; i++) sum += ne_len[J.row0 + i];
+                J.cap = (int32_t)std::max<int64_t>(sum, 1);
+                J.scratch = scratch;
+                scratch += (3ll * J.n * J.cap + 255) & ~255ll;
+                max_cap = std::max<int>(max_cap, J.cap);
+            }
+        }
+        const int nj = (int)todo.size();
+        al->d_scratch.ensure((size_t)std::max<int64_t>(scratch, 256));
+        NPGX_HIP(hipMemcpyAsync(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob),
+                                hipMemcpyHostToDevice, st));
+        NPGX_HIP(hipMemcpyAsync(al->d_order.p, todo.data(), todo.size() * 4, hipMemcpyHostToDevice, st));
+        NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
+        // per-slot scratch: word table, append_aligned stack, regions
+        const size_t slots = (size_t)std::max(1, std::min(nj, 2048));
+        uint32_t tlog = 10;
+        while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
+        const size_t tcap = (size_t)1 << tlog;
+        const int depth = max_len / std::max(1, o.aligned_check + 1) + 4;
+        if (slots * tcap > al->tcap_alloc || slots > al->slots_alloc || tcap != al->tcap_cur) {
+            al->tkeys.ensure(slots * tcap);
+            al->tmask.ensure(slots * tcap);
+            al->slot_epoch.ensure(slots);
+            NPGX_HIP(hipMemsetAsync(al->tkeys.p, 0, al->tkeys.cap * 8, st));
+            NPGX_HIP(hipMemsetAsync(al->slot_epoch.p, 0, al->slot_epoch.cap * 4, st));
+            al->tcap_alloc = std::max(al->tcap_alloc, slots * tcap);
+            al->slots_alloc = std::max(al->slots_alloc, slots);
+            al->tcap_cur = tcap;
+        }
+        al->st_p.ensure(slots * depth * 64);
+        al->st_len.ensure(slots * depth * 64);
+        al->st_pos.ensure(slots * depth * 64);
+        al->st_col.ensure(slots * depth);
+        al->regions.ensure(slots * (size_t)(max_cap + 1));
+        al->good_col.ensure(slots * (size_t)(max_cap + 1));
+
+        SaArgs A;
+        A.rows = al->d_rows.p;
+        A.row_off = al->d_row_off.p;
+        A.row_len = al->d_row_len.p;
+        A.jobs = al->d_jobs.p;
+        A.order = al->d_order.p;
+        A.n_jobs = nj;
+        A.aligner_type = o.aligner_type;
+        A.scratch = al->d_scratch.p;
+        A.job_len = al->d_job_len.p;
+        A.job_status = al->d_job_status.p;
+        A.next_job = al->d_next.p;
+        A.tkeys = al->tkeys.p;
+        A.tmask = al->tmask.p;
+        A.tcap_log2 = tlog;
+        A.slot_epoch = al->slot_epoch.p;
+        A.st_p = al->st_p.p;
+        A.st_len = al->st_len.p;
+        A.st_pos = al->st_pos.p;
+        A.st_col = al->st_col.p;
+        A.st_depth_max = depth;
+        A.regions = al->regions.p;
+        A.good_col = al->good_col.p;
+        A.slot_cols = max_cap + 1;
+        A.P = P;
+        int64_t residues = 0;
+        for (int32_t j : todo)
+            for (int i = 0; i < jobs[j].n; i++) residues += ne_len[jobs[j].row0 + i];
+        size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
+                                    double(residues) * 2.0, residues);
+        hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), 0, st, A);
+        NPGX_HIP(hipGetLastError());
+        al->timer.end(ti, st);
+        NPGX_HIP(hipMemcpyAsync(jlen.data(), al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipMemcpyAsync(jstat.data(), al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipStreamSynchronize(st));
+        std::vector<int32_t> again;
+        for (int32_t j : todo)
+            if (jstat[j] != 0) again.push_back(j);
+        if (attempt == 1 && !again.empty())
+            throw Error(NPGX_ERR_RANGE, "alignment exceeded the proven column bound");
+        // gather the finished jobs' rows (empty rows become all-gap rows)
+        std::vector<GatherRow> g;
+        std::vector<int64_t> g_row;
+        int64_t tot = 0;
+        for (int32_t j : todo) {
+            if (jstat[j] != 0) continue;
+            al->job_len[j] = jlen[j];
+            for (int64_t r = job_row_start[j]; r < job_row_start[j + 1]; r++) {
+                GatherRow x;
+                x.len = jlen[j];
+                x.pad = 0;
+                x.out_off = tot;
+                const int64_t ne = row_ne[r - r_base];
+                x.src = ne < 0 ? -1
+                               : jobs[j].scratch +
+                                     (int64_t)(jobs[j].n + (ne - jobs[j].row0)) * jobs[j].cap;
+                tot += x.len;
+                g.push_back(x);
+                g_row.push_back(r - r_base);
+            }
+        }
+        if (!g.empty()) {
+            al->d_gather.ensure(g.size());
+            al->d_out.ensure((size_t)std::max<int64_t>(tot, 1));
+            NPGX_HIP(hipMemcpyAsync(al->d_gather.p, g.data(), g.size() * sizeof(GatherRow),
+                                    hipMemcpyHostToDevice, st));
+            size_t tg = al->timer.begin("gather_rows", st, double(tot) * 2.0, tot);
+            hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)g.size()), dim3(64), 0, st, al->d_gather.p,
+                               (int64_t)g.size(), al->d_scratch.p, al->d_out.p);
+            NPGX_HIP(hipGetLastError());
+            al->timer.end(tg, st);
+            std::vector<char> part((size_t)std::max<int64_t>(tot, 1));
+            NPGX_HIP(hipMemcpyAsync(part.data(), al->d_out.p, (size_t)tot, hipMemcpyDeviceToHost, st));
+            NPGX_HIP(hipStreamSynchronize(st));
+            for (size_t i = 0; i < g.size(); i++)
+                row_out[g_row[i]].assign(part.data() + g[i].out_off, (size_t)g[i].len);
+        }
+        todo.swap(again);
+    }
+    // final layout: rows in input order
+    al->out_off.assign((size_t)std::max<int64_t>(n_rows, 0) + 1, 0);
+    int64_t off = 0;
+    for (int64_t r = 0; r < n_rows; r++) {
+        al->out_off[r] = off;
+        off += (int64_t)row_out[r].size();
+    }
+    al->out_off[n_rows] = off;
+    al->out.resize((size_t)std::max<int64_t>(off, 1));
+    for (int64_t r = 0; r < n_rows; r++)
+        memcpy(al->out.data() + al->out_off[r], row_out[r].data(), row_out[r].size());
+    al->has_result = true;
+}
+
+}  // namespace npgx
+
+extern "C" {
+
+void npgx_align_default_options(npgx_align_options* o) {
+    if (!o) return;
+    memset(o, 0, sizeof(*o));
+    o->mismatch_check = 1;        // MISMATCH_CHECK
+    o->gap_check = 2;             // GAP_CHECK
+    o->aligned_check = 10;        // ALIGNED_CHECK
+    o->min_length = 100;          // MIN_LENGTH
+    o->min_identity_x1e4 = 9000;  // MIN_IDENTITY 0.9
+    o->aligner_type = 0;
+    o->refine = 0;
+}
+
+int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
+    return guard([&] {
+        NPGX_REQUIRE(o && out, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(o->mismatch_check >= 0 && o->gap_check >= 1 && o->aligned_check >= 1 &&
+                         o->aligned_check <= 16 && o->min_length >= 0,
+                     NPGX_ERR_ARG, "aligner option out of range");
+        NPGX_REQUIRE(o->aligner_type == 0 || o->aligner_type == 1, NPGX_ERR_ARG, "unknown aligner type");
+        NPGX_REQUIRE(o->refine == 0, NPGX_ERR_ARG, "refine_alignment is not available yet");
+        int dev = current_device_checked();
+        auto* a = new npgx_aligner;
+        a->opt = *o;
+        a->device = dev;
+        if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete a;
+            throw Error(NPGX_ERR_HIP, "stream creation failed");
+        }
+        *out = a;
+    });
+}
+
+int npgx_align_batch(npgx_aligner* a, const char* rows, const int64_t* row_off,
+                     const int32_t* job_row_start, int32_t n_jobs) {
+    return guard([&] {
+        NPGX_REQUIRE(a && (n_jobs == 0 || (rows && row_off && job_row_start)), NPGX_ERR_ARG,
+                     "null argument");
+        align_batch(a, rows, row_off, job_row_start, n_jobs);
+    });
+}
+
+int npgx_align_result_sizes(const npgx_aligner* a, int64_t* total_bytes) {
+    return guard([&] {
+        NPGX_REQUIRE(a && total_bytes, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(a->has_result, NPGX_ERR_STATE, "no alignment result yet");
+        *total_bytes = a->out_off.empty() ? 0 : a->out_off.back();
+    });
+}
+
+int npgx_align_result_copy(const npgx_aligner* a, char* out, int64_t* out_off, int64_t* job_len) {
+    return guard([&] {
+        NPGX_REQUIRE(a, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(a->has_result, NPGX_ERR_STATE, "no alignment result yet");
+        if (out && !a->out_off.empty()) memcpy(out, a->out.data(), (size_t)a->out_off.back());
+        if (out_off) memcpy(out_off, a->out_off.data(), a->out_off.size() * 8);
+        if (job_len) memcpy(job_len, a->job_len.data(), a->job_len.size() * 8);
+    });
+}
+
+int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_t cap, int32_t* n) {
+    return guard([&] {
+        NPGX_REQUIRE(a && n && (out || cap == 0), NPGX_ERR_ARG, "null argument");
+        a->timer.copy_out(out, cap, n);
+    });
+}
+
+void npgx_aligner_free(npgx_aligner* a) {
+    if (!a) return;
+    (void)hipSetDevice(a->device);
+    if (a->stream) (void)hipStreamDestroy(a->stream);
+    delete a;
+}
+
+}  // extern "C"

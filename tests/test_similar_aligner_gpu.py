@@ -1,0 +1,139 @@
+"""SimilarAligner / DummyAligner parity: batched HIP kernel (through the C ABI)
+vs the CPU restatement of AbstractAligner::align_seqs (bit-exact rows).
+
+Cases: the reference's own tests (src/test/similar_aligner.cpp, aligner.cpp,
+test-lua/aligner-remove-gaps.lua) and seeded random families of rows built the
+way FragmentsExtender flanks look: mutated copies of a common ancestor
+(substitutions, indels, N runs), with homology that may end part-way, plus
+unrelated rows, empty rows and single rows.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+KATS = [
+    ["ATTT", "ANTT", "ATTT"],
+    ["ATGC", "AGC", "ATGC"],
+    ["CCCATATGG", "CCATATCG"],
+    ["ACCAGCTTTCGACCGCGGTGGCGATCGCGATATTAG", "ACCAGCTGGTGGCGATCGCGATATTAG",
+     "ACCAGCTTTCGACCGCGGTGGCGATCGCGATATTAG"],
+    ["ATG", "AG", ""],
+    ["ATG", "AG"],
+    ["CGAAT", "CAAAT"],
+    ["GTTT", "GTTTT"],
+    ["GCTATAAAGCAGCCTTCTTAGCTCACC", "ACTTGATGTGCGGCTCGGGATATTTCA",
+     "CCCTCTCTGGGCAGGGCGAACATTAAA", "TTGTAATGCTATTCCATAGTGAGATGA"],
+    ["AGAGCGGTTCCGGCGATTCCGTT", "AGAGCGATTCCGTT"],
+    ["TTATGAGTCGAGAATATGGTGCCAAAGT", "TTATGAGTCGAGATATGGTGCCAAAGT"],
+    ["AT", "A"], ["AT", "T"], ["", ""], ["A"], ["ACGT"], ["", "ACGT", ""],
+]
+
+
+def _aligner(kind="similar"):
+    from npge_amd.aligner import BatchAligner
+    return BatchAligner(kind)
+
+
+def _family(rng, n, length, d, indel=0.1, tail_unrelated=0.0, nrate=0.0):
+    anc = rng.integers(0, 4, length)
+    rows = []
+    for _ in range(n):
+        out = []
+        i = 0
+        cut = length if rng.random() >= tail_unrelated else int(rng.integers(0, length + 1))
+        while i < length:
+            if i >= cut:
+                out.append(int(rng.integers(0, 4)))
+                i += 1
+                continue
+            r = rng.random()
+            if r < d * (1 - indel):
+                out.append((int(anc[i]) + int(rng.integers(1, 4))) % 4)
+                i += 1
+            elif r < d:
+                k = int(rng.integers(1, 6))
+                if rng.random() < 0.5:
+                    out.extend(int(x) for x in rng.integers(0, 4, k))
+                else:
+                    i += k
+            else:
+                out.append(int(anc[i]))
+                i += 1
+        s = "".join("ATGC"[x] for x in out)
+        if nrate and rng.random() < nrate and len(s) > 10:
+            a = int(rng.integers(0, len(s) - 5))
+            s = s[:a] + "N" * 5 + s[a + 5:]
+        rows.append(s)
+    return rows
+
+
+def _random_jobs(seed, count, nmax=20, lmax=300):
+    rng = np.random.default_rng(seed)
+    jobs = []
+    for _ in range(count):
+        n = int(rng.integers(1, nmax + 1))
+        L = int(rng.integers(0, lmax + 1))
+        d = float(rng.choice([0.0, 0.005, 0.02, 0.05, 0.15, 0.4]))
+        jobs.append(_family(rng, n, L, d, tail_unrelated=float(rng.choice([0.0, 0.5])),
+                            nrate=float(rng.choice([0.0, 0.3]))))
+    return jobs
+
+
+def _check(jobs, kind="similar"):
+    mode = "align_seqs" if kind == "similar" else "dummy"
+    got = _aligner(kind).align(jobs)
+    for job, g in zip(jobs, got):
+        exp = orc.align(job, mode=mode)
+        assert g == exp, (job, g, exp)
+
+
+def test_kats_similar():
+    _check(KATS)
+
+
+def test_kats_expected_rows():
+    got = _aligner().align([["ATGC", "AGC", "ATGC"], ["ATG", "AG"], ["AT", "A"], ["AT", "T"]])
+    assert got[0] == ["ATGC", "A-GC", "ATGC"]
+    assert got[1] == ["ATG", "A-G"]
+    assert got[2] == ["AT", "A-"]          # AbstractAligner::test (aligner.cpp:14-28)
+    assert got[3] == ["AT", "-T"]
+
+
+def test_kats_dummy():
+    got = _aligner("dummy").align([["A-T-G-CATG", "ACT-GTCAT-"], ["AT", "A"], ["AT", "T"]])
+    assert got[0] == ["A-TG-CATG", "ACTGTCAT-"]   # similar_aligner.cpp aligner_remove_gap_cols
+    assert got[1] == ["AT", "A-"]
+    assert got[2] == ["AT", "T-"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_families(seed):
+    _check(_random_jobs(seed, 150))
+
+
+def test_long_flanks():
+    _check(_random_jobs(11, 40, nmax=17, lmax=1500))
+
+
+def test_wide_blocks():
+    _check(_random_jobs(12, 20, nmax=64, lmax=200))
+
+
+def test_unrelated_rows():
+    rng = np.random.default_rng(7)
+    jobs = [["".join("ATGC"[x] for x in rng.integers(0, 4, int(rng.integers(50, 400))))
+             for _ in range(int(rng.integers(2, 10)))] for _ in range(30)]
+    _check(jobs)
+
+
+def test_dummy_random():
+    _check(_random_jobs(5, 50), kind="dummy")
+
+
+def test_too_many_rows_rejected():
+    from npge_amd import _capi
+    with pytest.raises(_capi.NpgxError):
+        _aligner().align([["ACGT"] * 65])

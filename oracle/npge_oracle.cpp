@@ -26,6 +26,7 @@
 #include <cstring>
 #include <map>
 #include <set>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -947,6 +948,761 @@ static void refine_alignment(Strings& a) {
     remove_pure_gaps(a);
 }
 
+
+// ============================================================================
+// Block-set model and the DraftPangenome block build (lua_lib.lua:1569-1621)
+// ============================================================================
+struct BSeq {
+    std::string name, data, genome;
+    int index;
+};
+
+// A fragment with an optional gapped row.  Letters of the row are always the
+// fragment's own text in its orientation (Fragment::print_contents,
+// Fragment.cpp:344-372).
+struct BFrag {
+    int seq;
+    int64_t min, max;
+    int ori;
+    std::string row;  // empty = no row
+    bool has_row = false;
+    int64_t length() const { return max - min + 1; }
+    int64_t begin() const { return ori == 1 ? min : max; }
+    int64_t last() const { return ori == 1 ? max : min; }
+};
+
+struct BBlock {
+    std::vector<BFrag> f;
+    std::string name;
+    int64_t aln_len() const {
+        if (f.empty()) return 0;
+        return f[0].has_row ? (int64_t)f[0].row.size() : f[0].length();
+    }
+};
+
+struct BlockSetO {
+    std::vector<BSeq>* seqs;
+    std::vector<BBlock> blocks;
+};
+
+// Sequence::substr_impl (Sequence.cpp:310-325): ori -1 walks down and complements
+static std::string seq_substr(const BSeq& s, int64_t index, int64_t length, int ori) {
+    std::string r;
+    r.reserve((size_t)length);
+    for (int64_t i = 0; i < length; i++) {
+        char c = s.data[(size_t)index];
+        if (ori == -1) c = complement_char(c);
+        r += c;
+        index += ori;
+    }
+    return r;
+}
+
+static std::string frag_text(const std::vector<BSeq>& seqs, const BFrag& f) {
+    return seq_substr(seqs[f.seq], f.begin(), f.length(), f.ori);
+}
+
+// Fragment::str() with gap '-' (row) or plain text
+static std::string frag_str(const std::vector<BSeq>& seqs, const BFrag& f) {
+    if (f.has_row) return f.row;
+    return frag_text(seqs, f);
+}
+
+// Fragment::id (Fragment.cpp:173-183)
+static std::string frag_id(const std::vector<BSeq>& seqs, const BFrag& f, bool inv = false) {
+    int ori = inv ? -f.ori : f.ori;
+    int64_t a = ori == 1 ? f.min : f.max, b = ori == 1 ? f.max : f.min;
+    if (a == b && ori == -1) b = -1;
+    return seqs[f.seq].name + "_" + std::to_string(a) + "_" + std::to_string(b);
+}
+
+// block_hash (block_hash.cpp:29-55)
+static uint64_t block_hash(const std::vector<BSeq>& seqs, const BBlock& b) {
+    std::vector<std::string> d, v;
+    for (const BFrag& f : b.f) {
+        d.push_back(frag_id(seqs, f));
+        v.push_back(frag_id(seqs, f, true));
+    }
+    std::sort(d.begin(), d.end());
+    std::sort(v.begin(), v.end());
+    const std::vector<std::string>& ids = (d < v) ? d : v;
+    std::string joint;
+    for (size_t i = 0; i < ids.size(); i++) {
+        if (i) joint += ' ';
+        joint += ids[i];
+    }
+    size_t ns = (joint.size() + 15) / 16 * 16;
+    joint.resize(ns, ' ');
+    uint64_t a = 1;
+    for (size_t i = 0; i < ns / 16; i++) {
+        uint64_t v0, v1;
+        memcpy(&v0, joint.data() + 16 * i, 8);
+        memcpy(&v1, joint.data() + 16 * i + 8, 8);
+        a *= v0;
+        a ^= v1;
+    }
+    return a;
+}
+
+// blockset_hash (block_hash.cpp:112-130): XOR over blocks of size > 1
+static uint64_t blockset_hash(const BlockSetO& bs) {
+    uint64_t h = 0;
+    for (const BBlock& b : bs.blocks)
+        if (b.f.size() > 1) h ^= block_hash(*bs.seqs, b);
+    return h;
+}
+
+// ---------------------------------------------------------------- aligners as processors
+// AbstractAligner::alignment_needed + align_block (AbstractAligner.cpp:51-69,145-177)
+static void align_block(const std::vector<BSeq>& seqs, BBlock& b, int aligner,
+                        const SimilarAlignerImpl& im) {
+    if (b.f.empty()) return;
+    if (b.f.size() == 1) {
+        BFrag& f = b.f[0];
+        if (f.has_row && (int64_t)f.row.size() == f.length()) return;
+        f.row = frag_text(seqs, f);
+        f.has_row = true;
+        return;
+    }
+    if (b.f[0].has_row) {
+        size_t L = b.f[0].row.size();
+        bool all = true;
+        for (const BFrag& f : b.f)
+            if (!f.has_row || f.row.size() != L) { all = false; break; }
+        if (all) return;
+    }
+    Strings rows;
+    for (const BFrag& f : b.f) rows.push_back(frag_text(seqs, f));  // str(gap = 0)
+    align_seqs(rows, aligner, im);
+    refine_alignment(rows);
+    for (size_t i = 0; i < b.f.size(); i++) {
+        b.f[i].row = rows[i];
+        b.f[i].has_row = true;
+    }
+}
+
+// ---------------------------------------------------------------- FragmentsExtender
+// FragmentsExtender.cpp:34-119
+static int max_right_shift(const std::vector<BSeq>& seqs, const BFrag& f) {
+    if (f.ori == 1) return (int)seqs[f.seq].data.size() - 1 - (int)f.max;
+    return (int)f.min;
+}
+
+static void extend_right(const std::vector<BSeq>& seqs, BBlock& b, std::vector<std::string>& out,
+                         int extend_length, const SimilarAlignerImpl& im, int64_t* aligned) {
+    int rl = max_right_shift(seqs, b.f[0]);
+    for (const BFrag& f : b.f) rl = std::min(rl, max_right_shift(seqs, f));
+    rl = std::min(rl, extend_length);
+    out.assign(b.f.size(), std::string());
+    if (rl == 0) return;
+    Strings rows;
+    for (BFrag& f : b.f) {
+        int64_t start = f.length();
+        // Fragment::substr(start, stop) -> seq substr from frag_to_seq(start)
+        int64_t sp = f.begin() + f.ori * start;
+        rows.push_back(seq_substr(seqs[f.seq], sp, rl, f.ori));
+        if (f.ori == 1) f.max += rl;  // shift_end
+        else f.min -= rl;
+    }
+    if (aligned) for (auto& r : rows) *aligned += (int64_t)r.size();
+    align_seqs(rows, 0, im);
+    for (size_t i = 0; i < rows.size(); i++) out[i].swap(rows[i]);
+}
+
+static void fragments_extender(const std::vector<BSeq>& seqs, BBlock& b, int extend_length_opt,
+                               int64_t portion_x1e4, const SimilarAlignerImpl& im,
+                               int64_t* aligned) {
+    if (b.f.size() < 2 || !b.f[0].has_row) return;
+    std::vector<std::string> central;
+    for (const BFrag& f : b.f) central.push_back(frag_str(seqs, f));
+    int64_t length = b.aln_len();
+    // (portion * length).to_i() with Decimal arithmetic
+    int64_t portion_length = (portion_x1e4 * (length * 10000) / 10000) / 10000;
+    int extend_length = (int)std::max<int64_t>(extend_length_opt, portion_length);
+    std::vector<std::string> right, left;
+    extend_right(seqs, b, right, extend_length, im, aligned);
+    for (BFrag& f : b.f) f.ori = -f.ori;  // Block::inverse(false)
+    extend_right(seqs, b, left, extend_length, im, aligned);
+    for (BFrag& f : b.f) f.ori = -f.ori;
+    for (size_t i = 0; i < b.f.size(); i++) {
+        std::string l = left[i];
+        complement_str(l);
+        b.f[i].row = l + central[i] + right[i];
+        b.f[i].has_row = true;
+    }
+}
+
+// ---------------------------------------------------------------- FixEnds
+// is_ident_nogap (block_stat.cpp:156-169) on gapped rows
+static bool is_ident_nogap(const BBlock& b, int64_t col, bool reversed) {
+    char seen = 0;
+    const int64_t L = b.aln_len();
+    for (const BFrag& f : b.f) {
+        char c = f.row[(size_t)(reversed ? L - 1 - col : col)];
+        if (c == '-') return false;
+        if (reversed) c = complement_char(c);
+        if (seen == 0) seen = c;
+        else if (c != seen) return false;
+    }
+    return true;
+}
+
+// GoodAlnFinder (FixEnds.cpp:36-115)
+struct GoodAlnFinder {
+    const BBlock* block;
+    bool reversed;
+    std::vector<char> good_col;
+    int64_t length;
+    int min_fragment;
+    int min_good, sub_frame, good;
+    int64_t start, stop;
+    void init_frame() {
+        good_col.assign((size_t)min_fragment, 0);
+        good = 0;
+        for (int i = 0; i < min_fragment; i++) {
+            bool g = is_ident_nogap(*block, i, reversed);
+            good += g;
+            good_col[i] = g;
+        }
+        start = 0;
+        stop = min_fragment - 1;
+    }
+    void shift() {
+        bool g = is_ident_nogap(*block, stop, reversed);
+        char& c = good_col[(size_t)(stop % min_fragment)];
+        good -= c;
+        good += g;
+        c = g;
+    }
+    bool start_is_good() const { return good_col[(size_t)(start % min_fragment)]; }
+    bool find_first_good_frame() {
+        while (true) {
+            if (good >= min_good && start_is_good()) return true;
+            start += 1;
+            stop += 1;
+            if (stop >= length) return false;
+            shift();
+        }
+    }
+    int64_t find_start() {
+        if (length < min_fragment) return length;
+        init_frame();
+        if (!find_first_good_frame()) return length;
+        int best_score = good;
+        int64_t best_start = start;
+        while (true) {
+            start += 1;
+            stop += 1;
+            if (stop >= length) break;
+            shift();
+            bool ok = find_first_good_frame();
+            if (!ok || start - best_start > sub_frame) break;
+            if (good > best_score) {
+                best_score = good;
+                best_start = start;
+            }
+        }
+        return best_start;
+    }
+};
+
+// Block::slice with rows (Block.cpp:238-284): the letters of columns
+// [start, stop]; fragments with no letter there are dropped.
+static BBlock block_slice(const std::vector<BSeq>& seqs, const BBlock& b, int64_t start, int64_t stop) {
+    BBlock r;
+    for (const BFrag& f : b.f) {
+        int64_t before = 0, cnt = 0;
+        for (int64_t c = 0; c < start; c++) before += f.row[(size_t)c] != '-';
+        for (int64_t c = start; c <= stop; c++) cnt += f.row[(size_t)c] != '-';
+        if (cnt == 0) continue;
+        int64_t s_start = f.begin() + f.ori * before;
+        int64_t s_stop = f.begin() + f.ori * (before + cnt - 1);
+        BFrag nf;
+        nf.seq = f.seq;
+        if (s_start <= s_stop) {  // Fragment::set_begin_last (Fragment.cpp:111-121)
+            nf.min = s_start;
+            nf.max = s_stop;
+            nf.ori = 1;
+        } else {
+            nf.min = s_stop;
+            nf.max = s_start;
+            nf.ori = -1;
+        }
+        nf.row = f.row.substr((size_t)start, (size_t)(stop - start + 1));
+        nf.has_row = true;
+        if (nf.ori != f.ori) {
+            // single letter of an ori -1 fragment: set_begin_last makes it ori +1 and
+            // the row then shows the forward letter
+            for (char& c : nf.row)
+                if (c != '-') c = seqs[f.seq].data[(size_t)nf.min];
+        }
+        r.f.push_back(nf);
+    }
+    return r;
+}
+
+// FixEnds::process_block_impl (FixEnds.cpp:117-144): returns 0 keep, 1 replace, 2 drop
+static int fix_ends(const std::vector<BSeq>& seqs, const BBlock& b, int min_fragment,
+                    int64_t min_identity_x1e4, BBlock& out) {
+    GoodAlnFinder g;
+    g.block = &b;
+    g.length = b.aln_len();
+    g.min_fragment = min_fragment;
+    // (min_identity * min_fragment).to_i(), ((1 - min_identity) * min_fragment).to_i()
+    g.min_good = (int)((min_identity_x1e4 * ((int64_t)min_fragment * 10000) / 10000) / 10000);
+    g.sub_frame = (int)(((10000 - min_identity_x1e4) * ((int64_t)min_fragment * 10000) / 10000) / 10000);
+    g.reversed = false;
+    int64_t sd = g.find_start();
+    g.reversed = true;
+    int64_t sr = g.find_start();
+    if (sd == 0 && sr == 0) return 0;
+    int64_t stop_direct = g.length - sr - 1;
+    int64_t slice_length = stop_direct - sd + 1;
+    if (slice_length >= min_fragment) {
+        out = block_slice(seqs, b, sd, stop_direct);
+        return 1;
+    }
+    return 2;
+}
+
+// ---------------------------------------------------------------- Filter
+static const int MAX_COLUMN_SCORE = 100;
+static const int LOG_SCORE[1000] = {
+#include "log_score.inc"
+};
+
+// goodColumns.cpp:10-31
+static bool isColumnGood(const Strings& rows, int64_t i) {
+    char first = rows[0][(size_t)i];
+    bool ok = true;
+    for (const auto& r : rows) ok &= r[(size_t)i] == first;
+    return ok && first != '-' && first != 'N';
+}
+static bool isColumnIdentGap(const Strings& rows, int64_t i) {
+    bool gap = false;
+    int A = 0, T = 0, G = 0, C = 0, N = 0;
+    for (const auto& r : rows) {
+        char l = r[(size_t)i];
+        gap |= l == '-';
+        A |= l == 'A';
+        T |= l == 'T';
+        G |= l == 'G';
+        C |= l == 'C';
+        N |= l == 'N';
+    }
+    return gap && (A + T + G + C == 1) && !N;
+}
+// goodColumns.cpp:150-209
+static void mapGap(std::vector<int>& sc, int64_t start, int64_t length, int min_identity, int min_length) {
+    int64_t end = start + length;
+    if (length >= 1000) length = 999;
+    int score = LOG_SCORE[length];
+    score = (score == MAX_COLUMN_SCORE) ? score : (score * min_identity / MAX_COLUMN_SCORE);
+    if (length >= min_length) score = -100 * MAX_COLUMN_SCORE;
+    for (int64_t i = start; i < end; i++) sc[(size_t)i] = score;
+}
+static std::vector<int> goodColumns(const Strings& rows, int64_t length, int min_identity, int min_length) {
+    if (min_length == -1) min_length = (int)length;
+    if (min_identity == -1) min_identity = MAX_COLUMN_SCORE;
+    std::vector<int> sc((size_t)length, 0);
+    int64_t gap_length = 0;
+    for (int64_t i = 0; i < length; i++) {
+        bool good = isColumnGood(rows, i);
+        bool ig = isColumnIdentGap(rows, i);
+        if (good) sc[(size_t)i] = MAX_COLUMN_SCORE;
+        if (ig) gap_length += 1;
+        else if (gap_length > 0) {
+            mapGap(sc, i - gap_length, gap_length, min_identity, min_length);
+            gap_length = 0;
+        }
+    }
+    if (gap_length > 0) mapGap(sc, length - gap_length, gap_length, min_identity, min_length);
+    return sc;
+}
+
+typedef std::pair<int64_t, int64_t> SS;
+// goodSlices.cpp:17-245
+struct GoodSlicer {
+    std::vector<int> score;
+    std::vector<int64_t> ssum, gsum;
+    int64_t frame_length, end_length, frame_score, end_score, block_length, min_length;
+    int min_identity;
+    GoodSlicer(const std::vector<int>& sc, int64_t fl, int64_t el, int mi, int64_t ml) : score(sc) {
+        block_length = (int64_t)sc.size();
+        frame_length = std::min(fl, block_length);
+        end_length = el;
+        frame_score = frame_length * mi;
+        end_score = el * mi;
+        min_length = ml;
+        min_identity = mi;
+        ssum.assign((size_t)block_length + 1, 0);
+        gsum.assign((size_t)block_length + 1, 0);
+        for (int64_t i = 0; i < block_length; i++) {
+            ssum[i + 1] = ssum[i] + sc[i];
+            int v = (sc[i] == MAX_COLUMN_SCORE) ? MAX_COLUMN_SCORE : std::min(sc[i], 0);
+            gsum[i + 1] = gsum[i] + v;
+        }
+    }
+    int64_t countScore(int64_t a, int64_t b) const { return ssum[b + 1] - ssum[a]; }
+    int64_t countGapless(int64_t a, int64_t b) const { return gsum[b + 1] - gsum[a]; }
+    bool goodSlice(int64_t start) const { return countScore(start, start + frame_length - 1) >= frame_score; }
+    bool goodLeftEnd(int64_t start) const {
+        return score[start] == MAX_COLUMN_SCORE && countGapless(start, start + end_length - 1) >= end_score;
+    }
+    bool goodRightEnd(int64_t stop) const {
+        return score[stop] == MAX_COLUMN_SCORE && countGapless(stop - end_length + 1, stop) >= end_score;
+    }
+    static int64_t len(const SS& s) { return s.second - s.first + 1; }
+    static bool overlaps(const SS& a, const SS& o) {
+        if (o.first <= a.first && a.first <= o.second) return true;
+        if (a.first <= o.first && o.first <= a.second) return true;
+        return false;
+    }
+    static SS exclude(const SS& a, const SS& o) {
+        int64_t s1 = a.first, e1 = a.second;
+        if (o.first <= a.first && a.first <= o.second) s1 = o.second + 1;
+        if (o.first <= a.second && a.second <= o.second) e1 = o.first - 1;
+        return SS(s1, e1);
+    }
+    bool valid(const SS& s) const { return len(s) >= min_length && s.first >= 0 && s.second < block_length; }
+    SS strip(const SS& s) const {
+        if (!valid(s)) return s;
+        int64_t a = s.first, b = s.second;
+        while (!goodLeftEnd(a) && a + end_length - 1 < b) a++;
+        while (!goodRightEnd(b) && a + end_length - 1 < b) b--;
+        return SS(a, b);
+    }
+    bool goodFrame(const SS& s) const {
+        if (len(s) >= frame_length) return true;
+        return countScore(s.first, s.second) >= (int64_t)min_identity * len(s);
+    }
+    bool goodEnds(const SS& s) const { return goodLeftEnd(s.first) && goodRightEnd(s.second) && goodFrame(s); }
+    std::vector<SS> joinedSlices() const {
+        std::vector<SS> s0;
+        bool prev = false;
+        for (int64_t i = 0; i <= block_length - frame_length; i++) {
+            bool cur = goodSlice(i);
+            if (cur) {
+                if (prev) s0.back().second += 1;
+                else s0.push_back(SS(i, i + frame_length - 1));
+            }
+            prev = cur;
+        }
+        std::vector<SS> out;
+        for (const SS& s : s0) {
+            SS t = strip(s);
+            if (valid(t)) out.push_back(t);
+        }
+        return out;
+    }
+    std::vector<SS> calculate() const {
+        if (min_length > block_length || min_length <= 0) return {};
+        if (frame_length > block_length || frame_length <= 0) return {};
+        if (end_length > min_length || end_length < 0) return {};
+        std::vector<SS> slices = joinedSlices(), result;
+        while (!slices.empty()) {
+            SS sel = slices.front();
+            for (const SS& s : slices)
+                if (len(s) > len(sel)) sel = s;
+            if (valid(sel) && goodEnds(sel)) {
+                result.push_back(sel);
+                std::vector<SS> n;
+                for (const SS& s : slices) {
+                    if (!overlaps(s, sel)) n.push_back(s);
+                    else {
+                        SS t = strip(exclude(s, sel));
+                        if (valid(t) && goodEnds(t)) n.push_back(t);
+                    }
+                }
+                slices.swap(n);
+            } else {
+                break;
+            }
+        }
+        return result;
+    }
+};
+
+struct FilterOpts {
+    int min_fragment = 100, min_block = 2, max_block = -1, frame_length = 100, min_end = 10;
+    int64_t min_identity_x1e4 = 9000;
+    bool find_subblocks = true;
+};
+
+static int min_ident_count(int64_t mi) {  // Filter.cpp:112-120
+    int64_t v = mi * 100 * 10000 / 10000;  // Decimal * 100
+    int r = (int)(v / 10000);
+    if (v % 10000) r += 1;
+    return r;
+}
+
+static std::vector<SS> good_subblocks(const std::vector<BSeq>& seqs, const BBlock& b, const FilterOpts& o) {
+    Strings rows;
+    for (const BFrag& f : b.f) rows.push_back(frag_str(seqs, f));
+    int64_t length = b.aln_len();
+    int mi = min_ident_count(o.min_identity_x1e4);
+    std::vector<int> sc = goodColumns(rows, length, mi, o.min_fragment);
+    GoodSlicer gs(sc, o.frame_length, o.min_end, mi, o.min_fragment);
+    return gs.calculate();
+}
+
+static bool frag_valid(const std::vector<BSeq>& seqs, const BFrag& f) {
+    return f.min <= f.max && f.max < (int64_t)seqs[f.seq].data.size();
+}
+
+// Filter::is_good_block (Filter.cpp:143-174)
+static bool filter_is_good(const std::vector<BSeq>& seqs, const BBlock& b, const FilterOpts& o) {
+    int64_t L = b.aln_len();
+    if (L < o.min_fragment) return false;
+    for (const BFrag& f : b.f)
+        if (!frag_valid(seqs, f)) return false;
+    if ((int)b.f.size() < o.min_block) return false;
+    if (o.max_block != -1 && (int)b.f.size() > o.max_block) return false;
+    bool all_rows = true;
+    for (const BFrag& f : b.f) all_rows &= f.has_row;
+    if (all_rows && o.min_identity_x1e4 > 500) {
+        std::vector<SS> sl = good_subblocks(seqs, b, o);
+        if (!(sl.size() == 1 && sl[0] == SS(0, L - 1))) return false;
+    }
+    return true;
+}
+
+// Filter::find_good_subblocks (Filter.cpp:176-196)
+static void filter_subblocks(const std::vector<BSeq>& seqs, const BBlock& b, const FilterOpts& o,
+                             std::vector<BBlock>& out) {
+    if ((int)b.f.size() < o.min_block) return;
+    for (const BFrag& f : b.f)
+        if (!f.has_row) return;
+    if (b.aln_len() < o.min_fragment) return;
+    for (const SS& s : good_subblocks(seqs, b, o)) out.push_back(block_slice(seqs, b, s.first, s.second));
+}
+
+// Filter::process_block_impl (Filter.cpp:208-248): 0 keep, 1 replaced by out, 2 drop
+static int filter_block(const std::vector<BSeq>& seqs, BBlock& b, const FilterOpts& o,
+                        std::vector<BBlock>& out) {
+    if (filter_is_good(seqs, b, o)) return 0;
+    std::vector<BBlock> sub;
+    if (o.find_subblocks) filter_subblocks(seqs, b, o, sub);
+    if (!sub.empty()) {
+        for (auto& x : sub) out.push_back(x);
+        return 1;
+    }
+    std::vector<BFrag> kept;
+    for (const BFrag& f : b.f)
+        if (frag_valid(seqs, f)) kept.push_back(f);
+    if (kept.size() != b.f.size()) {
+        b.f = kept;
+        if (filter_is_good(seqs, b, o)) return 0;
+        if (o.find_subblocks) filter_subblocks(seqs, b, o, out);
+        return out.empty() ? 2 : 1;
+    }
+    return 2;
+}
+
+// ---------------------------------------------------------------- ExtendLoopFast driver
+struct PipelineOpts {
+    SimilarAlignerImpl im;
+    int extend_length = 100;            // MIN_LENGTH
+    int64_t portion_x1e4 = 5000;        // --extend-length-portion:=0.5
+    int fix_min_fragment = 100;
+    int64_t fix_min_identity_x1e4 = 9000;
+    int max_iterations = 10;
+    FilterOpts filter;
+    bool do_filter = true;
+};
+
+// RemoveNonStem --exact (RemoveNonStem.cpp:29-45)
+static void remove_non_stem(BlockSetO& bs, bool exact) {
+    std::set<std::string> genomes;
+    for (const BSeq& s : *bs.seqs) genomes.insert(s.genome);
+    std::vector<BBlock> keep;
+    for (BBlock& b : bs.blocks) {
+        std::set<std::string> g;
+        bool ok = true;
+        for (const BFrag& f : b.f) {
+            const std::string& gn = (*bs.seqs)[f.seq].genome;
+            if (exact && g.count(gn)) { ok = false; break; }
+            g.insert(gn);
+        }
+        if (ok)
+            for (const std::string& gn : genomes)
+                if (!g.count(gn)) { ok = false; break; }
+        if (ok) keep.push_back(std::move(b));
+    }
+    bs.blocks.swap(keep);
+}
+
+// pinned order for OverlaplessUnion (OverlaplessUnion.cpp:25-32 + block_less ties)
+static bool frag_less(const BFrag& a, const BFrag& b) {  // Fragment::operator< (seq* -> index)
+    if (a.min != b.min) return a.min < b.min;
+    if (a.max != b.max) return a.max < b.max;
+    if (a.ori != b.ori) return a.ori < b.ori;
+    return a.seq < b.seq;
+}
+static const BFrag& min_frag(const BBlock& b) {
+    size_t k = 0;
+    for (size_t i = 1; i < b.f.size(); i++)
+        if (frag_less(b.f[i], b.f[k])) k = i;
+    return b.f[k];
+}
+static bool ou_before(const BBlock& a, const BBlock& b) {
+    if (a.f.size() != b.f.size()) return a.f.size() > b.f.size();
+    if (a.aln_len() != b.aln_len()) return a.aln_len() > b.aln_len();
+    if (a.name != b.name) return a.name > b.name;
+    if (a.f.empty()) return false;
+    const BFrag& x = min_frag(a);
+    const BFrag& y = min_frag(b);
+    if (frag_less(x, y)) return true;
+    if (frag_less(y, x)) return false;
+    // final pin: sorted fragment lists
+    std::vector<std::tuple<int64_t, int64_t, int, int>> fa, fb;
+    for (const BFrag& f : a.f) fa.emplace_back(f.min, f.max, f.ori, f.seq);
+    for (const BFrag& f : b.f) fb.emplace_back(f.min, f.max, f.ori, f.seq);
+    std::sort(fa.begin(), fa.end());
+    std::sort(fb.begin(), fb.end());
+    return fa < fb;
+}
+
+// SetFc::has_overlap (FragmentCollection.hpp:273-297): neighbours in a
+// per-sequence set ordered by Fragment::operator<
+struct FragSetCmp {
+    bool operator()(const BFrag& a, const BFrag& b) const { return frag_less(a, b); }
+};
+struct OverlapIndex {
+    std::map<int, std::multiset<BFrag, FragSetCmp>> m;
+    static bool common(const BFrag& a, const BFrag& b) {
+        return a.seq == b.seq && std::max(a.min, b.min) <= std::min(a.max, b.max);
+    }
+    bool has_overlap(const BFrag& f) const {
+        auto it = m.find(f.seq);
+        if (it == m.end() || it->second.empty()) return false;
+        auto i2 = it->second.lower_bound(f);
+        if (i2 != it->second.end() && common(*i2, f)) return true;
+        if (i2 != it->second.begin()) {
+            --i2;
+            if (common(*i2, f)) return true;
+        }
+        return false;
+    }
+    bool block_has_overlap(const BBlock& b) const {
+        for (const BFrag& f : b.f)
+            if (has_overlap(f)) return true;
+        return false;
+    }
+    void add(const BBlock& b) {
+        for (const BFrag& f : b.f) m[f.seq].insert(f);
+    }
+};
+
+struct PipelineStats {
+    int iterations = 0;
+    int64_t aligned_residues = 0;   // flank residues sent to the aligner
+    int64_t anchor_blocks = 0, stem_blocks = 0;
+};
+
+// ExtendLoopFast (lua_lib.lua:697-709) under Pipe::run_impl (Pipe.cpp:60-78)
+static void extend_loop_fast(BlockSetO& bs, const PipelineOpts& o, PipelineStats& st) {
+    const std::vector<BSeq>& seqs = *bs.seqs;
+    std::set<uint64_t> seen_states;
+    seen_states.insert(blockset_hash(bs));
+    std::vector<uint64_t> mu_hashes;  // MoveUnchanged::hashes_ (sorted)
+    for (int it = 0; it < o.max_iterations || o.max_iterations == -1; it++) {
+        st.iterations++;
+        // MoveUnchanged target=unchanged other=target
+        std::vector<BBlock> unchanged, work;
+        std::vector<uint64_t> fresh;
+        for (BBlock& b : bs.blocks) {
+            uint64_t h = block_hash(seqs, b);
+            if (std::binary_search(mu_hashes.begin(), mu_hashes.end(), h)) unchanged.push_back(std::move(b));
+            else {
+                fresh.push_back(h);
+                work.push_back(std::move(b));
+            }
+        }
+        for (uint64_t h : fresh) mu_hashes.push_back(h);
+        std::sort(mu_hashes.begin(), mu_hashes.end());
+        mu_hashes.erase(std::unique(mu_hashes.begin(), mu_hashes.end()), mu_hashes.end());
+        // ExtendAndFix: FragmentsExtender --extend-length-portion:=0.5, FixEnds
+        for (BBlock& b : work)
+            fragments_extender(seqs, b, o.extend_length, o.portion_x1e4, o.im, &st.aligned_residues);
+        std::vector<BBlock> fixed;
+        for (BBlock& b : work) {
+            if (b.f.empty() || !b.f[0].has_row) {  // FixEnds asserts alignment; anchors have rows
+                fixed.push_back(std::move(b));
+                continue;
+            }
+            BBlock out;
+            int r = fix_ends(seqs, b, o.fix_min_fragment, o.fix_min_identity_x1e4, out);
+            if (r == 0) fixed.push_back(std::move(b));
+            else if (r == 1) fixed.push_back(std::move(out));
+        }
+        // Move target=target other=unchanged
+        for (BBlock& b : unchanged) fixed.push_back(std::move(b));
+        // OverlaplessUnion target=ol other=target --ou-move:=1
+        std::vector<size_t> order(fixed.size());
+        for (size_t i = 0; i < order.size(); i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](size_t a, size_t b) { return ou_before(fixed[a], fixed[b]); });
+        OverlapIndex idx;
+        std::vector<BBlock> ol;
+        for (size_t i : order) {
+            if (!idx.block_has_overlap(fixed[i])) {
+                idx.add(fixed[i]);
+                ol.push_back(std::move(fixed[i]));
+            }
+        }
+        // Clear target; Move target=target other=ol; Clear ol
+        bs.blocks.swap(ol);
+        uint64_t h = blockset_hash(bs);
+        if (seen_states.count(h)) break;
+        seen_states.insert(h);
+    }
+}
+
+// DraftPangenome without the random genome subset (ngenomes = all):
+// AnchorFinder -> RemoveNonStem --exact -> DummyAligner -> ExtendLoopFast(10) -> Filter
+static void draft_pangenome(std::vector<BSeq>& seqs, AnchorFinder& af, const PipelineOpts& o,
+                            BlockSetO& bs, PipelineStats& st) {
+    std::vector<Seq> all(seqs.size());
+    for (size_t i = 0; i < seqs.size(); i++) {
+        all[i].name = seqs[i].name;
+        all[i].data = seqs[i].data;
+        all[i].index = (int)i;
+    }
+    AnchorResult ar;
+    af.run(all, ar);
+    bs.seqs = &seqs;
+    bs.blocks.clear();
+    for (size_t b = 0; b + 1 < ar.block_start.size(); b++) {
+        BBlock blk;
+        for (int64_t i = ar.block_start[b]; i < ar.block_start[b + 1]; i++) {
+            BFrag f;
+            f.seq = ar.frag_seq[i];
+            f.min = ar.frag_min[i];
+            f.max = ar.frag_max[i];
+            f.ori = ar.frag_ori[i];
+            blk.f.push_back(f);
+        }
+        bs.blocks.push_back(blk);
+    }
+    st.anchor_blocks = (int64_t)bs.blocks.size();
+    remove_non_stem(bs, true);
+    st.stem_blocks = (int64_t)bs.blocks.size();
+    for (BBlock& b : bs.blocks) align_block(seqs, b, 1, o.im);  // DummyAligner
+    extend_loop_fast(bs, o, st);
+    if (o.do_filter) {
+        std::vector<BBlock> out;
+        for (BBlock& b : bs.blocks) {
+            std::vector<BBlock> sub;
+            int r = filter_block(seqs, b, o.filter, sub);
+            if (r == 0) out.push_back(std::move(b));
+            else if (r == 1)
+                for (auto& x : sub) out.push_back(std::move(x));
+        }
+        bs.blocks.swap(out);
+    }
+}
+
 }  // namespace orc
 
 // ============================================================================
@@ -1085,5 +1841,176 @@ int orc_align(int nrows, const char* rows, const int64_t* lens, const int32_t* p
     for (int i = 0; i < nrows; i++) memcpy(out + (int64_t)i * L, seqs[i].data(), (size_t)L);
     return 0;
 }
+
+// --- block-set processors and the DraftPangenome pipeline ----------------------
+struct orc_bs {
+    std::vector<orc::BSeq> seqs;
+    orc::BlockSetO bs;
+    orc::PipelineStats st;
+    orc::AnchorFinder af;
+    orc::PipelineOpts po;
+};
+
+// params (int64): [0] extend_length, [1] portion_x1e4, [2] fix_min_fragment,
+// [3] fix_min_identity_x1e4, [4] max_iterations, [5] filter.min_fragment,
+// [6] filter.min_block, [7] filter.frame_length, [8] filter.min_end,
+// [9] filter.min_identity_x1e4, [10] filter.find_subblocks, [11] do_filter,
+// [12..16] aligner (mismatch, gap, aligned, min_length, min_identity_x1e4),
+// [17] anchor_size, [18] anchor_fp_x1e4, [19] max_anchor_fragments, [20] seed,
+// [21] filter.max_block
+orc_bs* orc_bs_create(int nseq, const char* const* seqs, const int64_t* lens,
+                      const char* const* names, const int64_t* prm) {
+    orc_bs* h = new orc_bs;
+    h->seqs.resize((size_t)nseq);
+    for (int i = 0; i < nseq; i++) {
+        h->seqs[i].name = names[i];
+        h->seqs[i].data = orc::to_atgcn(std::string(seqs[i], (size_t)lens[i]));
+        h->seqs[i].genome = orc::genome_of(names[i]);
+        h->seqs[i].index = i;
+    }
+    h->bs.seqs = &h->seqs;
+    orc::PipelineOpts& o = h->po;
+    o.extend_length = (int)prm[0];
+    o.portion_x1e4 = prm[1];
+    o.fix_min_fragment = (int)prm[2];
+    o.fix_min_identity_x1e4 = prm[3];
+    o.max_iterations = (int)prm[4];
+    o.filter.min_fragment = (int)prm[5];
+    o.filter.min_block = (int)prm[6];
+    o.filter.frame_length = (int)prm[7];
+    o.filter.min_end = (int)prm[8];
+    o.filter.min_identity_x1e4 = prm[9];
+    o.filter.find_subblocks = prm[10] != 0;
+    o.do_filter = prm[11] != 0;
+    o.im.mismatch_check = (int)prm[12];
+    o.im.gap_check = (int)prm[13];
+    o.im.aligned_check = (int)prm[14];
+    o.im.min_length = (int)prm[15];
+    o.im.min_identity_x1e4 = prm[16];
+    h->af.anchor = (int)prm[17];
+    h->af.fp_x1e4 = prm[18];
+    h->af.max_anchor_fragments = prm[19];
+    h->af.seed = (uint32_t)prm[20];
+    o.filter.max_block = (int)prm[21];
+    return h;
+}
+void orc_bs_free(orc_bs* h) { delete h; }
+
+// replace the block set: fragments in block order; rows optional (row_len[i] < 0: none)
+void orc_bs_set_blocks(orc_bs* h, int64_t nb, const int64_t* block_start, const int32_t* seq,
+                       const int64_t* mn, const int64_t* mx, const int32_t* ori,
+                       const int64_t* row_off, const int64_t* row_len, const char* rows) {
+    h->bs.blocks.clear();
+    for (int64_t b = 0; b < nb; b++) {
+        orc::BBlock blk;
+        for (int64_t i = block_start[b]; i < block_start[b + 1]; i++) {
+            orc::BFrag f;
+            f.seq = seq[i];
+            f.min = mn[i];
+            f.max = mx[i];
+            f.ori = ori[i];
+            if (row_len && row_len[i] >= 0) {
+                f.row.assign(rows + row_off[i], (size_t)row_len[i]);
+                f.has_row = true;
+            }
+            blk.f.push_back(f);
+        }
+        h->bs.blocks.push_back(blk);
+    }
+}
+
+// op: 0 FragmentsExtender, 1 FixEnds, 2 Filter, 3 ExtendLoopFast, 4 DummyAligner,
+// 5 RemoveNonStem --exact, 6 DraftPangenome (AnchorFinder on all sequences first),
+// 7 MetaAligner(similar) align_block
+int orc_bs_apply(orc_bs* h, int op) {
+    const std::vector<orc::BSeq>& seqs = h->seqs;
+    orc::PipelineOpts& o = h->po;
+    std::vector<orc::BBlock> out;
+    switch (op) {
+        case 0:
+            for (auto& b : h->bs.blocks)
+                orc::fragments_extender(seqs, b, o.extend_length, o.portion_x1e4, o.im,
+                                        &h->st.aligned_residues);
+            return 0;
+        case 1:
+            for (auto& b : h->bs.blocks) {
+                orc::BBlock x;
+                int r = orc::fix_ends(seqs, b, o.fix_min_fragment, o.fix_min_identity_x1e4, x);
+                if (r == 0) out.push_back(b);
+                else if (r == 1) out.push_back(x);
+            }
+            h->bs.blocks.swap(out);
+            return 0;
+        case 2:
+            for (auto& b : h->bs.blocks) {
+                std::vector<orc::BBlock> sub;
+                int r = orc::filter_block(seqs, b, o.filter, sub);
+                if (r == 0) out.push_back(b);
+                else if (r == 1)
+                    for (auto& x : sub) out.push_back(x);
+            }
+            h->bs.blocks.swap(out);
+            return 0;
+        case 3:
+            orc::extend_loop_fast(h->bs, o, h->st);
+            return 0;
+        case 4:
+            for (auto& b : h->bs.blocks) orc::align_block(seqs, b, 1, o.im);
+            return 0;
+        case 5:
+            orc::remove_non_stem(h->bs, true);
+            return 0;
+        case 6:
+            orc::draft_pangenome(h->seqs, h->af, o, h->bs, h->st);
+            return 0;
+        case 7:
+            for (auto& b : h->bs.blocks) orc::align_block(seqs, b, 0, o.im);
+            return 0;
+        case 8:  // Filter::find_good_subblocks only
+            for (auto& b : h->bs.blocks) orc::filter_subblocks(seqs, b, o.filter, out);
+            h->bs.blocks.swap(out);
+            return 0;
+    }
+    return -1;
+}
+
+// [n_blocks, n_fragments, row_bytes, iterations, aligned_residues, anchor_blocks, stem_blocks]
+void orc_bs_counts(const orc_bs* h, int64_t* c) {
+    int64_t nf = 0, rb = 0;
+    for (const auto& b : h->bs.blocks) {
+        nf += (int64_t)b.f.size();
+        for (const auto& f : b.f) rb += (int64_t)f.row.size();
+    }
+    c[0] = (int64_t)h->bs.blocks.size();
+    c[1] = nf;
+    c[2] = rb;
+    c[3] = h->st.iterations;
+    c[4] = h->st.aligned_residues;
+    c[5] = h->st.anchor_blocks;
+    c[6] = h->st.stem_blocks;
+}
+
+void orc_bs_copy(const orc_bs* h, int64_t* block_start, int32_t* seq, int64_t* mn, int64_t* mx,
+                 int32_t* ori, int64_t* row_off, int64_t* row_len, char* rows) {
+    int64_t k = 0, ro = 0;
+    size_t b = 0;
+    for (; b < h->bs.blocks.size(); b++) {
+        block_start[b] = k;
+        for (const auto& f : h->bs.blocks[b].f) {
+            seq[k] = f.seq;
+            mn[k] = f.min;
+            mx[k] = f.max;
+            ori[k] = f.ori;
+            row_off[k] = ro;
+            row_len[k] = f.has_row ? (int64_t)f.row.size() : -1;
+            memcpy(rows + ro, f.row.data(), f.row.size());
+            ro += (int64_t)f.row.size();
+            k++;
+        }
+    }
+    block_start[b] = k;
+}
+
+uint64_t orc_bs_hash(const orc_bs* h) { return orc::blockset_hash(h->bs); }
 
 }  // extern "C"

@@ -197,3 +197,117 @@ def align(rows, mode="similar", params=DEFAULT_SA, return_past_end=False):
     Ln = out_len.value
     res = [out[i * Ln:(i + 1) * Ln].tobytes().decode() for i in range(len(rows))]
     return (res, pe.value) if return_past_end else res
+
+
+# ---------------------------------------------------------------- block sets
+PIPELINE_DEFAULTS = dict(
+    extend_length=100, portion_x1e4=5000, fix_min_fragment=100, fix_min_identity_x1e4=9000,
+    max_iterations=10, filter_min_fragment=100, filter_min_block=2, filter_frame_length=100,
+    filter_min_end=10, filter_min_identity_x1e4=9000, filter_find_subblocks=1, do_filter=1,
+    mismatch_check=1, gap_check=2, aligned_check=10, min_length=100, min_identity_x1e4=9000,
+    anchor_size=20, anchor_fp_x1e4=1000, max_anchor_fragments=100000, seed=1,
+    filter_max_block=-1)
+_PKEYS = list(PIPELINE_DEFAULTS)
+
+OPS = {"FragmentsExtender": 0, "FixEnds": 1, "Filter": 2, "ExtendLoopFast": 3, "DummyAligner": 4,
+       "RemoveNonStem": 5, "DraftPangenome": 6, "MetaAligner": 7, "FindGoodSubblocks": 8}
+
+
+def _bs_lib():
+    L = lib()
+    if not getattr(L, "_bs_bound", False):
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        L.orc_bs_create.argtypes = [ctypes.c_int, vp, vp, vp, vp]
+        L.orc_bs_create.restype = vp
+        L.orc_bs_free.argtypes = [vp]
+        L.orc_bs_set_blocks.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.orc_bs_apply.argtypes = [vp, ctypes.c_int]
+        L.orc_bs_apply.restype = ctypes.c_int
+        L.orc_bs_counts.argtypes = [vp, vp]
+        L.orc_bs_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.orc_bs_hash.argtypes = [vp]
+        L.orc_bs_hash.restype = ctypes.c_uint64
+        L._bs_bound = True
+    return L
+
+
+class BlockSetOracle:
+    """Oracle block set: sequences + blocks, with the hot-path processors
+    (FragmentsExtender, FixEnds, Filter, ExtendLoopFast, DummyAligner,
+    RemoveNonStem, DraftPangenome)."""
+
+    def __init__(self, seqs, names, **params):
+        L = _bs_lib()
+        p = dict(PIPELINE_DEFAULTS)
+        p.update(params)
+        prm = np.array([p[k] for k in _PKEYS], dtype=np.int64)
+        n = len(seqs)
+        bufs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
+        arr = (ctypes.c_char_p * max(n, 1))(*bufs)
+        lens = np.array([len(b) for b in bufs] or [0], dtype=np.int64)
+        nm = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in names])
+        self._h = L.orc_bs_create(n, ctypes.cast(arr, ctypes.c_void_p), _ptr(lens),
+                                  ctypes.cast(nm, ctypes.c_void_p), _ptr(prm))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _bs_lib().orc_bs_free(self._h)
+            self._h = None
+
+    def set_blocks(self, blocks):
+        """blocks: list of lists of (seq_index, min, max, ori, row_or_None)."""
+        frs = [f for b in blocks for f in b]
+        bs = np.zeros(len(blocks) + 1, dtype=np.int64)
+        np.cumsum([len(b) for b in blocks], out=bs[1:])
+        seq = np.array([f[0] for f in frs] or [0], dtype=np.int32)
+        mn = np.array([f[1] for f in frs] or [0], dtype=np.int64)
+        mx = np.array([f[2] for f in frs] or [0], dtype=np.int64)
+        ori = np.array([f[3] for f in frs] or [0], dtype=np.int32)
+        rows = [(f[4] or "") for f in frs]
+        rl = np.array([len(f[4]) if f[4] is not None else -1 for f in frs] or [0], dtype=np.int64)
+        ro = np.zeros(max(len(frs), 1), dtype=np.int64)
+        if frs:
+            ro[1:len(frs)] = np.cumsum([len(r) for r in rows])[:-1]
+        data = "".join(rows).encode() or b"\0"
+        _bs_lib().orc_bs_set_blocks(self._h, len(blocks), _ptr(bs), _ptr(seq), _ptr(mn), _ptr(mx),
+                                    _ptr(ori), _ptr(ro), _ptr(rl), data)
+
+    def apply(self, op):
+        rc = _bs_lib().orc_bs_apply(self._h, OPS[op])
+        if rc != 0:
+            raise RuntimeError("oracle op %s failed" % op)
+        return self
+
+    def stats(self):
+        c = np.zeros(7, dtype=np.int64)
+        _bs_lib().orc_bs_counts(self._h, _ptr(c))
+        return dict(n_blocks=int(c[0]), n_fragments=int(c[1]), iterations=int(c[3]),
+                    aligned_residues=int(c[4]), anchor_blocks=int(c[5]), stem_blocks=int(c[6]))
+
+    def blocks(self):
+        L = _bs_lib()
+        c = np.zeros(7, dtype=np.int64)
+        L.orc_bs_counts(self._h, _ptr(c))
+        nb, nf, rbytes = int(c[0]), int(c[1]), int(c[2])
+        bs = np.zeros(nb + 1, dtype=np.int64)
+        seq = np.zeros(max(nf, 1), dtype=np.int32)
+        mn = np.zeros(max(nf, 1), dtype=np.int64)
+        mx = np.zeros(max(nf, 1), dtype=np.int64)
+        ori = np.zeros(max(nf, 1), dtype=np.int32)
+        ro = np.zeros(max(nf, 1), dtype=np.int64)
+        rl = np.zeros(max(nf, 1), dtype=np.int64)
+        rows = ctypes.create_string_buffer(max(rbytes, 1))
+        L.orc_bs_copy(self._h, _ptr(bs), _ptr(seq), _ptr(mn), _ptr(mx), _ptr(ori), _ptr(ro), _ptr(rl),
+                      ctypes.cast(rows, ctypes.c_void_p))
+        raw = rows.raw
+        out = []
+        for b in range(nb):
+            blk = []
+            for i in range(bs[b], bs[b + 1]):
+                row = raw[ro[i]:ro[i] + rl[i]].decode() if rl[i] >= 0 else None
+                blk.append((int(seq[i]), int(mn[i]), int(mx[i]), int(ori[i]), row))
+            out.append(blk)
+        return out
+
+    def hash(self):
+        return _bs_lib().orc_bs_hash(self._h)

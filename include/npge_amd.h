@@ -13,6 +13,7 @@
  *                   (src/model/Sequence.cpp:151-179,525-600; src/algo/SeqI.hpp:45-57)
  *   npgx_af_*       Processor "AnchorFinder" (src/algo/AnchorFinder.hpp:33-53,
  *                   AnchorFinder.cpp:37-53 options, :393-406 run_impl)
+ *   npgx_blockset_* Processor/BlockSet surface of the block build (below)
  *   npgx_align_*    AbstractAligner::align_seqs + SimilarAligner::similar_aligner
  *                   (src/algo/AbstractAligner.cpp:104-143,
  *                   src/algo/SimilarAligner.cpp:487-501), MetaAligner
@@ -130,7 +131,8 @@ void npgx_af_free(npgx_af* af);
  * (SimilarAligner) or "dummy" (DummyAligner).  A batch holds n_jobs independent
  * alignment problems (one per block); job j owns rows
  * [job_row_start[j], job_row_start[j+1]) and row r is the text
- * rows[row_off[r] .. row_off[r+1]).  Rows must be ATGCN upper/lower case.
+ * rows[row_off[r] .. row_off[r+1]).  Similar-aligner rows must be upper-case
+ * ATGCN (the sequences' to_atgcn alphabet); dummy rows may hold anything.
  * Options (SimilarAligner.cpp:503-516, CMakeLists.txt:35-37,55-60): */
 typedef struct {
     int32_t mismatch_check;     /* default 1 */
@@ -154,6 +156,69 @@ int npgx_align_result_copy(const npgx_aligner* a, char* out, int64_t* out_off,
 int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_t cap,
                             int32_t* n);
 void npgx_aligner_free(npgx_aligner* a);
+
+
+/* ------------------------------------------------------------------ block sets
+ * A block set over a sequence set: blocks of fragments (sequence input index,
+ * min_pos, max_pos, ori) with optional gapped rows ('-' = gap).  Processors run
+ * in place.  Names and semantics follow the reference processors:
+ *   "RemoveNonStem"      RemoveNonStem --exact (src/algo/RemoveNonStem.cpp:29-45)
+ *   "DummyAligner"       AbstractAligner::align_block with DummyAligner
+ *                        (AbstractAligner.cpp:51-69, DummyAligner.cpp:18-26)
+ *   "FragmentsExtender"  FragmentsExtender (src/algo/FragmentsExtender.cpp:87-119)
+ *   "FixEnds"            FixEnds (src/algo/FixEnds.cpp:117-144)
+ *   "ExtendLoopFast"     Pipe ExtendLoopFast (src/algo/lua_lib.lua:697-709,
+ *                        src/algo/Pipe.cpp:60-78)
+ *   "Filter"             Filter (src/algo/Filter.cpp:208-248)
+ *   "DraftPangenome"     AnchorFinder -> RemoveNonStem -> DummyAligner ->
+ *                        ExtendLoopFast -> Filter (lua_lib.lua:1569-1621) */
+typedef struct npgx_blockset npgx_blockset;
+
+typedef struct {
+    int32_t extend_length;          /* FragmentsExtender extend-length (MIN_LENGTH 100) */
+    int32_t max_iterations;         /* ExtendLoopFast iterations (DraftPangenome: 10) */
+    int64_t extend_portion_x1e4;    /* extend-length-portion (ExtendAndFix: 0.5) */
+    int32_t min_fragment;           /* FixEnds / Filter min-fragment (MIN_LENGTH) */
+    int32_t frame_length;           /* Filter frame-length (FRAME_LENGTH 100) */
+    int32_t min_end;                /* Filter min-end (MIN_END 10) */
+    int32_t min_block;              /* Filter min-block (2) */
+    int32_t max_block;              /* Filter max-block (-1) */
+    int32_t find_subblocks;         /* Filter find-subblocks (1) */
+    int64_t min_identity_x1e4;      /* FixEnds / Filter min-identity (MIN_IDENTITY 0.9) */
+    npgx_align_options align;       /* aligner used by FragmentsExtender */
+} npgx_bb_options;
+
+typedef struct {
+    int64_t iterations;             /* ExtendLoopFast iterations run */
+    int64_t aligned_residues;       /* flank residues sent to the aligner */
+    int64_t align_jobs;             /* alignment problems solved */
+    int64_t anchor_blocks;
+    int64_t stem_blocks;
+    double ms_align;                /* wall ms inside the GPU aligner */
+    double ms_host;                 /* wall ms of host bookkeeping */
+} npgx_bb_stats;
+
+void npgx_bb_default_options(npgx_bb_options* o);
+int npgx_blockset_create(const npgx_seqset* s, const npgx_bb_options* o, npgx_blockset** out);
+/* replace the blocks; row_off == NULL: no rows, else row i = rows[row_off[i]..row_off[i+1]) */
+int npgx_blockset_set_blocks(npgx_blockset* b, int64_t n_blocks, const int64_t* block_start,
+                             const int32_t* seq, const int64_t* min_pos, const int64_t* max_pos,
+                             const int8_t* ori, const int64_t* row_off, const char* rows);
+/* append the blocks found by the last npgx_af_run of af */
+int npgx_blockset_add_anchors(npgx_blockset* b, const npgx_af* af);
+/* run a processor by its reference name (see above); DraftPangenome uses af */
+int npgx_blockset_apply(npgx_blockset* b, const char* processor, npgx_af* af);
+int npgx_blockset_counts(const npgx_blockset* b, int64_t* n_blocks, int64_t* n_fragments,
+                         int64_t* row_bytes);
+int npgx_blockset_copy(const npgx_blockset* b, int64_t* block_start, int32_t* seq,
+                       int64_t* min_pos, int64_t* max_pos, int8_t* ori, int64_t* row_off,
+                       char* rows);
+/* blockset_hash (src/model/block_hash.cpp:112-130) */
+int npgx_blockset_hash(const npgx_blockset* b, uint64_t* hash);
+int npgx_blockset_stats(const npgx_blockset* b, npgx_bb_stats* out);
+int npgx_blockset_kernel_times(const npgx_blockset* b, npgx_kernel_time* out, int32_t cap,
+                               int32_t* n);
+void npgx_blockset_free(npgx_blockset* b);
 
 #ifdef __cplusplus
 }

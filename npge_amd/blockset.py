@@ -1,0 +1,156 @@
+"""Block-set processors on the engine (npgx_blockset_*).
+
+Mirrors the reference's BlockSet + per-block processors of the block build:
+RemoveNonStem, DummyAligner, FragmentsExtender, FixEnds, OverlaplessUnion,
+ExtendLoopFast, Filter and the DraftPangenome driver (lua_lib.lua:1569-1621).
+Alignment work goes to the HIP aligner in one batch per processor pass.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _capi
+
+
+class BbOptions(ctypes.Structure):
+    _fields_ = [("extend_length", ctypes.c_int32), ("max_iterations", ctypes.c_int32),
+                ("extend_portion_x1e4", ctypes.c_int64), ("min_fragment", ctypes.c_int32),
+                ("frame_length", ctypes.c_int32), ("min_end", ctypes.c_int32),
+                ("min_block", ctypes.c_int32), ("max_block", ctypes.c_int32),
+                ("find_subblocks", ctypes.c_int32), ("min_identity_x1e4", ctypes.c_int64),
+                ("align", _capi.AlignOptions)]
+
+
+class BbStats(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int64), ("aligned_residues", ctypes.c_int64),
+                ("align_jobs", ctypes.c_int64), ("anchor_blocks", ctypes.c_int64),
+                ("stem_blocks", ctypes.c_int64), ("ms_align", ctypes.c_double),
+                ("ms_host", ctypes.c_double)]
+
+
+def _bind(L):
+    if getattr(L, "_bb_bound", False):
+        return L
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    P = ctypes.POINTER
+    L.npgx_bb_default_options.argtypes = [P(BbOptions)]
+    L.npgx_bb_default_options.restype = None
+    L.npgx_blockset_create.argtypes = [vp, P(BbOptions), P(vp)]
+    L.npgx_blockset_set_blocks.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp]
+    L.npgx_blockset_add_anchors.argtypes = [vp, vp]
+    L.npgx_blockset_apply.argtypes = [vp, ctypes.c_char_p, vp]
+    L.npgx_blockset_counts.argtypes = [vp, P(i64), P(i64), P(i64)]
+    L.npgx_blockset_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
+    L.npgx_blockset_hash.argtypes = [vp, P(ctypes.c_uint64)]
+    L.npgx_blockset_stats.argtypes = [vp, P(BbStats)]
+    L.npgx_blockset_kernel_times.argtypes = [vp, P(_capi.KernelTime), ctypes.c_int32,
+                                             P(ctypes.c_int32)]
+    L.npgx_blockset_free.argtypes = [vp]
+    L.npgx_blockset_free.restype = None
+    L._bb_bound = True
+    return L
+
+
+ALIGN_KEYS = ("mismatch_check", "gap_check", "aligned_check", "align_min_length",
+              "align_min_identity_x1e4")
+
+
+def default_options(**kw):
+    L = _bind(_capi.lib())
+    o = BbOptions()
+    L.npgx_bb_default_options(ctypes.byref(o))
+    for k, v in kw.items():
+        if k in ALIGN_KEYS:
+            setattr(o.align, k.replace("align_", ""), v)
+        else:
+            setattr(o, k, v)
+    return o
+
+
+class BlockSetEngine:
+    """One npgx_blockset over a device sequence set."""
+
+    def __init__(self, seqset, options=None, **kw):
+        L = _bind(_capi.lib())
+        self.ss = seqset
+        o = options or default_options(**kw)
+        h = ctypes.c_void_p()
+        _capi.check(L.npgx_blockset_create(seqset.handle, ctypes.byref(o), ctypes.byref(h)))
+        self._h = h
+
+    def set_blocks(self, blocks):
+        """blocks: list of lists of (seq_index, min, max, ori, row_or_None)."""
+        L = _capi.lib()
+        frs = [f for b in blocks for f in b]
+        bs = np.zeros(len(blocks) + 1, dtype=np.int64)
+        np.cumsum([len(b) for b in blocks], out=bs[1:])
+        seq = np.array([f[0] for f in frs] or [0], dtype=np.int32)
+        mn = np.array([f[1] for f in frs] or [0], dtype=np.int64)
+        mx = np.array([f[2] for f in frs] or [0], dtype=np.int64)
+        ori = np.array([f[3] for f in frs] or [1], dtype=np.int8)
+        has_rows = bool(frs) and frs[0][4] is not None
+        if has_rows:
+            rows = "".join(f[4] for f in frs).encode()
+            ro = np.zeros(len(frs) + 1, dtype=np.int64)
+            np.cumsum([len(f[4]) for f in frs], out=ro[1:])
+            buf = ctypes.create_string_buffer(rows, max(len(rows), 1))
+            _capi.check(L.npgx_blockset_set_blocks(self._h, len(blocks), _capi.ptr(bs), _capi.ptr(seq),
+                                                   _capi.ptr(mn), _capi.ptr(mx), _capi.ptr(ori),
+                                                   _capi.ptr(ro), ctypes.cast(buf, ctypes.c_void_p)))
+        else:
+            _capi.check(L.npgx_blockset_set_blocks(self._h, len(blocks), _capi.ptr(bs), _capi.ptr(seq),
+                                                   _capi.ptr(mn), _capi.ptr(mx), _capi.ptr(ori),
+                                                   None, None))
+        return self
+
+    def apply(self, processor, af=None):
+        L = _capi.lib()
+        afh = af._handle() if af is not None else None
+        _capi.check(L.npgx_blockset_apply(self._h, processor.encode(), afh))
+        return self
+
+    def blocks(self):
+        L = _capi.lib()
+        nb, nf, rb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _capi.check(L.npgx_blockset_counts(self._h, ctypes.byref(nb), ctypes.byref(nf), ctypes.byref(rb)))
+        n = max(nf.value, 1)
+        bs = np.zeros(nb.value + 1, dtype=np.int64)
+        seq = np.zeros(n, dtype=np.int32)
+        mn = np.zeros(n, dtype=np.int64)
+        mx = np.zeros(n, dtype=np.int64)
+        ori = np.zeros(n, dtype=np.int8)
+        ro = np.zeros(n + 1, dtype=np.int64)
+        rows = ctypes.create_string_buffer(max(rb.value, 1))
+        _capi.check(L.npgx_blockset_copy(self._h, _capi.ptr(bs), _capi.ptr(seq), _capi.ptr(mn),
+                                         _capi.ptr(mx), _capi.ptr(ori), _capi.ptr(ro),
+                                         ctypes.cast(rows, ctypes.c_void_p)))
+        raw = rows.raw
+        out = []
+        for b in range(nb.value):
+            blk = []
+            for i in range(bs[b], bs[b + 1]):
+                row = raw[ro[i]:ro[i + 1]].decode() if ro[i + 1] > ro[i] else None
+                blk.append((int(seq[i]), int(mn[i]), int(mx[i]), int(ori[i]), row))
+            out.append(blk)
+        return out
+
+    def hash(self):
+        h = ctypes.c_uint64()
+        _capi.check(_capi.lib().npgx_blockset_hash(self._h, ctypes.byref(h)))
+        return h.value
+
+    def stats(self):
+        st = BbStats()
+        _capi.check(_capi.lib().npgx_blockset_stats(self._h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in BbStats._fields_}
+
+    def kernel_times(self):
+        return _capi.kernel_times(_capi.lib().npgx_blockset_kernel_times, self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None:
+            try:
+                _capi.lib().npgx_blockset_free(self._h)
+            except Exception:
+                pass
+            self._h = None

@@ -10,8 +10,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libnpge_amd.so")
-SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip"]
-HEADERS = ["common.hpp", "sa_device.hpp"]
+SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip", "block_build.hip"]
+HEADERS = ["common.hpp", "sa_device.hpp", "log_score.inc"]
 ARCH = os.environ.get("NPGX_OFFLOAD_ARCH", "gfx950")
 
 

@@ -130,6 +130,12 @@ struct StageTimer {
 
 int current_device_checked();
 
+// similar_aligner.hip: batched align_seqs (results in the aligner's host buffers)
+void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
+                 const int32_t* job_row_start, int32_t n_jobs);
+const char* aligner_result(const npgx_aligner* al, const int64_t** row_off);
+std::string genome_of(const std::string& name);
+
 }  // namespace npgx
 
 // ----------------------------------------------------------------- sequence set

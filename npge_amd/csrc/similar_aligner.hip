@@ -409,7 +409,7 @@ struct npgx_aligner {
 
 namespace npgx {
 
-static void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
+void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
                         const int32_t* job_row_start, int32_t n_jobs) {
     NPGX_HIP(hipSetDevice(al->device));
     hipStream_t st = al->stream;
@@ -636,6 +636,11 @@ static void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_o
     for (int64_t r = 0; r < n_rows; r++)
         memcpy(al->out.data() + al->out_off[r], row_out[r].data(), row_out[r].size());
     al->has_result = true;
+}
+
+const char* aligner_result(const npgx_aligner* al, const int64_t** row_off) {
+    *row_off = al->out_off.data();
+    return al->out.data();
 }
 
 }  // namespace npgx

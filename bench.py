@@ -83,14 +83,19 @@ def main():
     value = total_bp / 1e6 / dt * args.steps
 
     # dominant kernel of the last step: algorithmic bytes / HIP-event duration
+    # (events recorded on the engine's own stream around each launch)
     kts = job.kernel_times()
     dom = max(kts, key=lambda k: k["ms"]) if kts else None
     roofline = None
     if dom and dom["ms"] > 0:
         ach = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom["name"],
-                    "kernel_ms": round(dom["ms"], 4), "bytes_per_launch": dom["bytes"]}
+        roofline = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "kernel": dom["name"],
+                    "launches_per_step": dom["launches"],
+                    "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
+                    "bytes_per_launch": dom["bytes"] / dom["launches"]}
+    kernels = sorted(({"name": k["name"], "ms": round(k["ms"], 4), "launches": k["launches"]}
+                      for k in kts), key=lambda k: -k["ms"])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -115,6 +120,7 @@ def main():
                        "anchor_fp": 0.1, "max_anchor_fragments": 100000,
                        "parallelism": "replica-per-gpu x%d" % world},
             "last_step": info,
+            "kernels_last_step": kernels,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -1,41 +1,50 @@
-"""Block-build driver for the benchmark and the smoke test.
-
-Round-1 state: the step is AnchorFinder on the device-resident genome set; the
-DraftPangenome block build after it (RemoveNonStem -> DummyAligner ->
-ExtendLoopFast -> Filter, src/algo/lua_lib.lua:1569-1621) is added stage by
-stage as its kernels reach parity (DESIGN.md "Status").
+"""Block-build driver used by bench.py and smoke(): one step = DraftPangenome on
+a device-resident genome set (AnchorFinder -> RemoveNonStem --exact ->
+DummyAligner -> ExtendLoopFast(10) -> Filter, src/algo/lua_lib.lua:1569-1621).
 """
 import time
 
 from .anchor_finder import AnchorFinder
+from .blockset import BlockSetEngine
+
+STAGES = ["AnchorFinder", "RemoveNonStem", "DummyAligner", "ExtendLoopFast(10)", "Filter"]
 
 
 class BlockBuild:
     def __init__(self, seqset, names, seqs, seed=1):
         self.ss = seqset
-        self.names = names
-        self.af = AnchorFinder()
-        self.af.set_opt_value("bloom-seed", seed)
-        self.stages = ["AnchorFinder"]
+        self.seed = seed
+        self.eng = BlockSetEngine(seqset)
+        self.af = None
 
     def workload_name(self, config):
-        return "%s: %s" % (config, " -> ".join(self.stages))
+        return "%s DraftPangenome: %s" % (config, " -> ".join(STAGES))
 
     def run(self):
-        # a fresh instance per step keeps every step identical (no used hashes)
+        # a fresh AnchorFinder per step: every step does identical work (no used hashes)
         self.af = AnchorFinder()
-        r = self.af.find(self.ss)
-        return {"anchor_blocks": int(len(r["block_start"]) - 1),
-                "anchor_fragments": int(len(r["seq"])), "collected": int(r["n_collected"]),
-                "found_fragments": int(r["n_found_frags"])}
+        self.af.set_opt_value("bloom-seed", self.seed)
+        self.eng.apply("DraftPangenome", af=self.af)
+        st = self.eng.stats()
+        return {"anchor_blocks": int(st["anchor_blocks"]), "stem_blocks": int(st["stem_blocks"]),
+                "iterations": int(st["iterations"]), "aligned_residues": int(st["aligned_residues"]),
+                "align_jobs": int(st["align_jobs"]), "ms_align_wall": round(st["ms_align"], 3),
+                "ms_host_bookkeeping": round(st["ms_host"], 3)}
 
     def kernel_times(self):
-        return self.af.kernel_times()
+        """Per-kernel totals of the last step: name -> (ms, bytes, launches)."""
+        agg = {}
+        for k in self.af.kernel_times() + self.eng.kernel_times():
+            a = agg.setdefault(k["name"], {"name": k["name"], "ms": 0.0, "bytes": 0.0, "launches": 0})
+            a["ms"] += k["ms"]
+            a["bytes"] += k["bytes"]
+            a["launches"] += 1
+        return list(agg.values())
 
 
 def cpu_reference_step(orc, names, seqs, seed=1):
     """Seconds for the same step on the CPU restatement (1 worker)."""
-    af = orc.AnchorFinder(seed=seed)
     t = time.perf_counter()
-    af.run(seqs, names)
+    o = orc.BlockSetOracle(seqs, names, seed=seed)
+    o.apply("DraftPangenome")
     return time.perf_counter() - t

@@ -155,6 +155,10 @@ int npgx_align_result_copy(const npgx_aligner* a, char* out, int64_t* out_off,
                            int64_t* job_len);
 int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_t cap,
                             int32_t* n);
+/* per job of the last batch, 8 int64: device cycles, alignment columns,
+ * try_aligned calls, shifts scanned, try_gap calls, FindLowSimilar regions,
+ * non-empty rows, wave slot */
+int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64_t* n);
 void npgx_aligner_free(npgx_aligner* a);
 
 
@@ -196,6 +200,10 @@ typedef struct {
     int64_t stem_blocks;
     double ms_align;                /* wall ms inside the GPU aligner */
     double ms_host;                 /* wall ms of host bookkeeping */
+    /* wall ms per stage of the last apply: 0 AnchorFinder, 1 RemoveNonStem +
+     * DummyAligner, 2 MoveUnchanged, 3 flank gather, 4 align batch, 5 stitch,
+     * 6 FixEnds, 7 OverlaplessUnion, 8 blockset hash, 9 Filter */
+    double ms_stage[12];
 } npgx_bb_stats;
 
 void npgx_bb_default_options(npgx_bb_options* o);
@@ -218,6 +226,9 @@ int npgx_blockset_hash(const npgx_blockset* b, uint64_t* hash);
 int npgx_blockset_stats(const npgx_blockset* b, npgx_bb_stats* out);
 int npgx_blockset_kernel_times(const npgx_blockset* b, npgx_kernel_time* out, int32_t cap,
                                int32_t* n);
+/* aligner per-job statistics of every batch of the last apply (8 int64 per job,
+ * layout of npgx_align_job_stats) */
+int npgx_blockset_job_stats(const npgx_blockset* b, int64_t* out, int64_t cap, int64_t* n);
 void npgx_blockset_free(npgx_blockset* b);
 
 #ifdef __cplusplus

@@ -25,7 +25,10 @@ class BbStats(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int64), ("aligned_residues", ctypes.c_int64),
                 ("align_jobs", ctypes.c_int64), ("anchor_blocks", ctypes.c_int64),
                 ("stem_blocks", ctypes.c_int64), ("ms_align", ctypes.c_double),
-                ("ms_host", ctypes.c_double)]
+                ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 12)]
+
+STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", "align_batch",
+               "stitch", "fix_ends", "overlapless_union", "blockset_hash", "filter"]
 
 
 def _bind(L):
@@ -45,6 +48,7 @@ def _bind(L):
     L.npgx_blockset_stats.argtypes = [vp, P(BbStats)]
     L.npgx_blockset_kernel_times.argtypes = [vp, P(_capi.KernelTime), ctypes.c_int32,
                                              P(ctypes.c_int32)]
+    L.npgx_blockset_job_stats.argtypes = [vp, vp, i64, P(i64)]
     L.npgx_blockset_free.argtypes = [vp]
     L.npgx_blockset_free.restype = None
     L._bb_bound = True
@@ -142,7 +146,19 @@ class BlockSetEngine:
     def stats(self):
         st = BbStats()
         _capi.check(_capi.lib().npgx_blockset_stats(self._h, ctypes.byref(st)))
-        return {k: getattr(st, k) for k, _ in BbStats._fields_}
+        d = {k: getattr(st, k) for k, _ in BbStats._fields_ if k != "ms_stage"}
+        d["ms_stage"] = {n: round(st.ms_stage[i], 3) for i, n in enumerate(STAGE_NAMES)}
+        return d
+
+    def job_stats(self):
+        """(n_jobs, 8) int64: cycles, columns, try_aligned calls, shifts, gaps,
+        regions, rows, slot of every alignment job of the last apply."""
+        L = _capi.lib()
+        n = ctypes.c_int64()
+        _capi.check(L.npgx_blockset_job_stats(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros((max(n.value, 1), 8), dtype=np.int64)
+        _capi.check(L.npgx_blockset_job_stats(self._h, _capi.ptr(out), n.value, ctypes.byref(n)))
+        return out[:n.value]
 
     def kernel_times(self):
         return _capi.kernel_times(_capi.lib().npgx_blockset_kernel_times, self._h)

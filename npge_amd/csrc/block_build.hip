@@ -85,6 +85,7 @@ struct npgx_blockset {
     npgx_bb_stats stats{};
     StageTimer timer;        // only host-visible timings are kept here
     std::vector<npgx_kernel_time> ktimes;
+    std::vector<int64_t> job_stats;  // aligner per-job statistics of the last apply
     const std::string& text(int32_t seq) const { return ss->data[(size_t)seq]; }
 };
 
@@ -101,6 +102,12 @@ static void collect_kernel_times(npgx_blockset* B) {
     int32_t n = 0;
     if (npgx_align_kernel_times(B->aligner, kt, 16, &n) == NPGX_OK)
         for (int32_t i = 0; i < std::min<int32_t>(n, 16); i++) B->ktimes.push_back(kt[i]);
+    int64_t nj = 0;
+    if (npgx_align_job_stats(B->aligner, nullptr, 0, &nj) == NPGX_OK && nj > 0) {
+        const size_t o = B->job_stats.size();
+        B->job_stats.resize(o + (size_t)nj * 8);
+        npgx_align_job_stats(B->aligner, B->job_stats.data() + o, nj, &nj);
+    }
 }
 
 // Fragment::id (Fragment.cpp:173-183)
@@ -308,6 +315,7 @@ static int max_right_shift(const npgx_blockset* B, const Frag& f, int ori) {
 
 static void fragments_extender(npgx_blockset* B, const std::vector<size_t>& which) {
     const int64_t portion = B->opt.extend_portion_x1e4;
+    auto tg = Clock::now();
     std::vector<FlankJob> jobs;
     std::string rows;
     std::vector<int64_t> row_off(1, 0);
@@ -338,6 +346,7 @@ static void fragments_extender(npgx_blockset* B, const std::vector<size_t>& whic
         }
     }
     // align every flank of every block in one batch
+    B->stats.ms_stage[3] += ms_since(tg);
     auto t0 = Clock::now();
     if (!jobs.empty()) {
         align_batch(B->aligner, rows.data(), row_off.data(), job_start.data(), (int32_t)jobs.size());
@@ -346,6 +355,8 @@ static void fragments_extender(npgx_blockset* B, const std::vector<size_t>& whic
         B->stats.align_jobs += (int64_t)jobs.size();
     }
     B->stats.ms_align += ms_since(t0);
+    B->stats.ms_stage[4] += ms_since(t0);
+    auto ts = Clock::now();
     const int64_t* ooff = nullptr;
     const char* out = jobs.empty() ? nullptr : aligner_result(B->aligner, &ooff);
     // stitch: revcomp(left) + central + right (FragmentsExtender.cpp:108-118)
@@ -371,6 +382,7 @@ static void fragments_extender(npgx_blockset* B, const std::vector<size_t>& whic
             b.rows[i].swap(row);
         }
     }
+    B->stats.ms_stage[5] += ms_since(ts);
 }
 
 // ---------------------------------------------------------------- FixEnds
@@ -577,6 +589,7 @@ static void extend_loop_fast(npgx_blockset* B) {
         std::sort(seen.begin(), seen.end());
         seen.erase(std::unique(seen.begin(), seen.end()), seen.end());
         B->stats.ms_host += ms_since(t0);
+        B->stats.ms_stage[2] += ms_since(t0);
         // ExtendAndFix: FragmentsExtender --extend-length-portion:=0.5, then FixEnds
         B->blocks.swap(work);
         std::vector<size_t> all(B->blocks.size());
@@ -584,10 +597,15 @@ static void extend_loop_fast(npgx_blockset* B) {
         fragments_extender(B, all);
         t0 = Clock::now();
         fix_ends(B, B->blocks);
+        B->stats.ms_stage[6] += ms_since(t0);
         // Move target=target other=unchanged; OverlaplessUnion --ou-move; Clear; Move
+        auto t1 = Clock::now();
         for (Block& b : unchanged) B->blocks.push_back(std::move(b));
         overlapless_union(B, B->blocks);
+        B->stats.ms_stage[7] += ms_since(t1);
+        auto t2 = Clock::now();
         const uint64_t h = blockset_hash(B);
+        B->stats.ms_stage[8] += ms_since(t2);
         B->stats.ms_host += ms_since(t0);
         if (states.count(h)) break;
         states.insert(h);
@@ -810,6 +828,7 @@ static void add_anchors(npgx_blockset* B, const npgx_af* af) {
 
 static void apply(npgx_blockset* B, const std::string& p, npgx_af* af) {
     B->ktimes.clear();
+    B->job_stats.clear();
     if (p == "RemoveNonStem") return remove_non_stem(B);
     if (p == "DummyAligner") return dummy_align(B);
     if (p == "FragmentsExtender") {
@@ -824,16 +843,21 @@ static void apply(npgx_blockset* B, const std::string& p, npgx_af* af) {
     if (p == "DraftPangenome") {
         NPGX_REQUIRE(af, NPGX_ERR_ARG, "DraftPangenome needs an AnchorFinder handle");
         B->stats = npgx_bb_stats{};
+        auto ta = Clock::now();
         if (npgx_af_run(af, B->ss) != NPGX_OK) throw Error(NPGX_ERR_HIP, npgx_last_error());
         B->blocks.clear();
         add_anchors(B, af);
+        B->stats.ms_stage[0] = ms_since(ta);
         B->stats.anchor_blocks = (int64_t)B->blocks.size();
+        auto tb = Clock::now();
         remove_non_stem(B);
         B->stats.stem_blocks = (int64_t)B->blocks.size();
         dummy_align(B);
+        B->stats.ms_stage[1] = ms_since(tb);
         extend_loop_fast(B);
         auto t0 = Clock::now();
         filter(B);
+        B->stats.ms_stage[9] = ms_since(t0);
         B->stats.ms_host += ms_since(t0);
         return;
     }
@@ -974,6 +998,14 @@ int npgx_blockset_kernel_times(const npgx_blockset* B, npgx_kernel_time* out, in
             out[k++] = t;
         }
         *n = (int32_t)B->ktimes.size();
+    });
+}
+
+int npgx_blockset_job_stats(const npgx_blockset* B, int64_t* out, int64_t cap, int64_t* n) {
+    return guard([&] {
+        NPGX_REQUIRE(B && n, NPGX_ERR_ARG, "null argument");
+        *n = (int64_t)B->job_stats.size() / 8;
+        if (out) memcpy(out, B->job_stats.data(), (size_t)std::min<int64_t>(cap, *n) * 64);
     });
 }
 

@@ -1,17 +1,22 @@
 // sa_device.hpp -- wave-level building blocks of the greedy multiple aligner
 // (SimilarAligner, src/algo/SimilarAligner.cpp:41-485) on CDNA4.
 //
-// One wavefront owns one alignment problem; lane i owns row i (n <= 64 rows).
-// A row is read through a View (char(q) = p[d*q] for q < len), so the reversed
-// sub-problems the reference creates with substr + std::reverse
-// (append_aligned :274-293) are views on the parent's rows, not copies.
-// Column tests (is_equal :101-115) are wave ballots.  The reference's recursion
-// (append_aligned -> process_seqs) runs on an explicit per-wave stack; a child
-// writes its output right after the parent's cursor and is reversed in place
-// when it returns.
+// One wavefront owns one alignment problem.  Two lane layouts alternate:
+//   * rows mode: lane i owns row i (n <= 64) -- pos and the view live in lane
+//     i's registers; column tests (is_equal :101-115) are ballots.  Used for the
+//     branchy steps: try_gap, try_aligned, the bookkeeping of append_end.
+//   * columns mode: lane j owns column pos+j of EVERY row; a 64-column chunk is
+//     read and written with coalesced byte accesses, one row at a time.  Used for
+//     the common case -- runs of identical columns and single mismatches
+//     (process_cols :355-358 with try_mismatch :122-134) -- and for bulk copies.
+// A row is read through a View (char(q) = p[d*q], q < len), so the reversed
+// sub-problems the reference builds with substr + std::reverse
+// (append_aligned :274-293) are views, not copies.  The recursion
+// append_aligned -> process_seqs runs on an explicit per-wave stack; a child
+// writes right after the parent's cursor and is reversed in place on return.
 //
 // Past-the-end reads (find_best_gap :191-217 may read beyond a row): char(len)
-// is '\0' like std::string; char(q > len) is a per-row sentinel that equals
+// is '\0' like std::string; char(q > len) is a per-row sentinel equal to
 // nothing (same convention as the oracle).
 #pragma once
 
@@ -30,23 +35,20 @@ struct View {
 
 struct Params {
     int mc, gc, ac, min_length;
-    int wf;                 // FindLowSimilar weight factor (FindLowSimilar.cpp:56-60)
+    int wf;  // FindLowSimilar weight factor (FindLowSimilar.cpp:56-60)
 };
 
 // Per-wave scratch (global memory), sized by the host for the batch.
 struct Slot {
-    unsigned long long* tkeys;   // try_aligned word table: (epoch << 48 | word)
-    unsigned long long* tmask;   // row masks
+    unsigned long long* tkeys;  // try_aligned word table: (epoch << 48 | word)
+    unsigned long long* tmask;  // row masks
     uint32_t tcap_log2;
-    uint32_t epoch;
-    // append_aligned stack: per level 64 lanes x {p, len|dneg<<31, pos} + uniform col
-    const char** st_p;
+    const char** st_p;          // append_aligned stack, 64 lanes per level
     int* st_len;
     int* st_pos;
     int* st_col;
     int st_depth_max;
-    // FindLowSimilar regions (start, stop, good, weight)
-    int4* regions;
+    int4* regions;              // FindLowSimilar regions (start, stop, good, weight)
     unsigned char* good_col;
 };
 
@@ -64,7 +66,6 @@ __device__ __forceinline__ int vch(const View& v, int q, int lane) {
     return q == v.len ? 0 : 0x100 + lane;  // q < 0 only on idle lanes (rows >= n)
 }
 
-// all active lanes agree on c
 __device__ __forceinline__ bool all_eq(const WaveCtx& w, int c) {
     const int c0 = __shfl(c, 0);
     return (ballot(!w.act || c == c0) & w.rowmask) == w.rowmask;
@@ -94,150 +95,268 @@ __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int s
     const unsigned hi = (unsigned)__shfl((int)(unsigned)(v >> 32), src);
     return ((unsigned long long)hi << 32) | lo;
 }
+__device__ __forceinline__ const char* shfl_ptr(const char* p, int src) {
+    return (const char*)shfl64((unsigned long long)p, src);
+}
 
-// Output buffer of one problem: row i at base + i*cap.
-struct Out {
-    char* base;
-    int cap;
-};
+// number of trailing one bits
+__device__ __forceinline__ int ctz_ones(unsigned long long m) {
+    return m == ~0ull ? 64 : __ffsll((long long)~m) - 1;
+}
 
-struct Frame {
-    View v;
-    int pos;
-};
+// ------------------------------------------------------------ columns-mode helpers
+// Buffers hold row r at base + r*cap.  All lanes take part; rows loop uniformly.
+
+// rows [0,n): dst[d0 + j] = src[s0 + j] for j < len
+__device__ __forceinline__ void cm_copy(const WaveCtx& w, const char* src, char* dst, int cap, int s0, int d0,
+                                        int len) {
+    for (int r = 0; r < w.n; r++) {
+        const char* a = src + (size_t)r * cap + s0;
+        char* b = dst + (size_t)r * cap + d0;
+        for (int j = w.lane; j < len; j += 64) b[j] = a[j];
+    }
+    __syncthreads();
+}
+
+// reverse columns [c0, c1) of every row in place
+__device__ __forceinline__ void cm_reverse(const WaveCtx& w, char* base, int cap, int c0, int c1) {
+    const int half = (c1 - c0) >> 1;
+    for (int r = 0; r < w.n; r++) {
+        char* row = base + (size_t)r * cap;
+        for (int j = w.lane; j < half; j += 64) {
+            const char x = row[c0 + j], y = row[c1 - 1 - j];
+            row[c0 + j] = y;
+            row[c1 - 1 - j] = x;
+        }
+    }
+    __syncthreads();
+}
 
 // ---------------------------------------------------------------- process_seqs
-// State of one process_seqs call tree (SimilarAligner.cpp:396-405) with the
-// append_aligned recursion flattened onto Slot's stack.
 struct Proc {
-    const WaveCtx& w;
-    const Params& P;
-    Slot& S;
-    Out out;
-    View v;
-    int pos;
-    int col;        // output cursor (all rows equal length between steps)
-    bool ovf;       // lane-local overflow
+    WaveCtx w;
+    Params P;
+    Slot S;
+    char* ob;        // output base (row r at ob + r*cap)
+    int cap;
+    View v;          // this lane's row (rows mode)
+    int pos;         // this lane's cursor
+    int col;         // output cursor (all rows equal length between steps)
+    bool ovf;
+    uint32_t epoch;  // word-table epoch (carried from one Proc to the next)
+    int n_aligned_calls, n_shifts, n_gaps, n_fast;
 
-    __device__ Proc(const WaveCtx& w_, const Params& P_, Slot& S_, Out o)
-        : w(w_), P(P_), S(S_), out(o), pos(0), col(0), ovf(false) {}
+    __device__ __forceinline__ Proc(const WaveCtx& w_, const Params& P_, const Slot& S_, char* ob_, int cap_,
+                                    uint32_t ep)
+        : w(w_), P(P_), S(S_), ob(ob_), cap(cap_), pos(0), col(0), ovf(false), epoch(ep), n_aligned_calls(0),
+          n_shifts(0), n_gaps(0), n_fast(0) {}
 
-    __device__ __forceinline__ void put(int c, char ch) {
-        if (c < out.cap) out.base[(size_t)w.lane * out.cap + c] = ch;
+    __device__ __forceinline__ void put(int c, char x) {
+        if (c < cap) ob[(size_t)w.lane * cap + c] = x;
         else ovf = true;
     }
     __device__ __forceinline__ int ch(int q) const { return vch(v, q, w.lane); }
+    __device__ __forceinline__ bool is_stop(int shift) const { return any_lane(w, pos + shift >= v.len); }
 
-    // is_stop :58-65
-    __device__ bool is_stop(int shift) const { return any_lane(w, pos + shift >= v.len); }
-
-    // append_cols :67-77
-    __device__ void append_cols(int cols) {
+    // append_cols :67-77 (rows mode, a few columns)
+    __device__ __forceinline__ void append_cols(int cols) {
         if (w.act)
             for (int j = 0; j < cols; j++) put(col + j, (char)ch(pos + j));
         pos += w.act ? cols : 0;
         col += cols;
     }
-    // append_all :91-99 (tail of every row, then append_gaps :79-89)
-    __device__ void append_all() {
-        int t = w.act ? v.len - pos : 0;
-        if (t < 0) t = 0;
-        const int m = wave_max(t);
-        if (w.act) {
-            for (int j = 0; j < t; j++) put(col + j, (char)ch(pos + j));
-            for (int j = t; j < m; j++) put(col + j, '-');
-            pos += t;
+
+    // every row's [pos, pos+t) then '-' up to m columns (columns mode);
+    // append_gaps :79-89 is the padding.  Advances pos by t and col by m.
+    __device__ __forceinline__ void write_tails(int t, int m) {
+        if (col + m > cap) {
+            ovf = true;
+            return;
         }
+        __syncthreads();
+        for (int r = 0; r < w.n; r++) {
+            const char* pr = shfl_ptr(v.p, r);
+            const int dr = __shfl(v.d, r), qr = __shfl(pos, r), tr = __shfl(t, r);
+            char* o = ob + (size_t)r * cap + col;
+            for (int j = w.lane; j < m; j += 64) o[j] = j < tr ? pr[(ptrdiff_t)dr * (qr + j)] : '-';
+        }
+        __syncthreads();
+        pos += w.act ? t : 0;
         col += m;
     }
-    // is_equal(pos + off, shift, cols) where off = 1 for lanes in `shifted`
-    __device__ bool is_equal_sh(unsigned long long shifted, int shift, int cols) const {
+    // append_all :91-99
+    __device__ __forceinline__ void append_all() {
+        int t = w.act ? v.len - pos : 0;
+        if (t < 0) t = 0;
+        write_tails(t, wave_max(t));
+    }
+
+    // Columns mode: consume the columns process_cols takes with is_equal /
+    // try_mismatch.  Returns 0: the next column needs a rows-mode step,
+    // 1: a row ended (is_stop(0) -> append_all).
+    __device__ __forceinline__ int fast_run() {
+        __syncthreads();
+        while (true) {
+            if (col + 64 > cap) return 0;  // near capacity: rows mode guards the writes
+            unsigned long long em, vm;
+            {
+                const int j = w.lane;
+                const char* p0 = shfl_ptr(v.p, 0);
+                const int d0 = __shfl(v.d, 0), l0 = __shfl(v.len, 0), q0 = __shfl(pos, 0);
+                bool valid = q0 + j < l0;
+                const char c0 = valid ? p0[(ptrdiff_t)d0 * (q0 + j)] : 0;
+                ob[col + j] = c0;  // speculative: columns past the consumed ones are rewritten later
+                bool eq = true;
+                for (int r = 1; r < w.n; r++) {
+                    const char* pr = shfl_ptr(v.p, r);
+                    const int dr = __shfl(v.d, r), lr = __shfl(v.len, r), qr = __shfl(pos, r);
+                    const bool vr = qr + j < lr;
+                    const char c = vr ? pr[(ptrdiff_t)dr * (qr + j)] : 0;
+                    ob[(size_t)r * cap + col + j] = c;
+                    valid &= vr;
+                    eq &= c == c0;
+                }
+                vm = ballot(valid);
+                em = ballot(valid && eq);
+            }
+            n_fast++;
+            int k = 0;
+            int ret = -1;  // -1: chunk consumed / restart, 0: rows step, 1: stop
+            while (true) {
+                const unsigned long long m = k == 0 ? em : ((em >> k) | (~0ull << (64 - k)));
+                k += ctz_ones(m);
+                if (k >= 64) {
+                    k = 64;
+                    break;
+                }
+                if (!((vm >> k) & 1ull)) {  // a row ends at column k
+                    ret = 1;
+                    break;
+                }
+                if (k + P.mc < 64) {  // try_mismatch: columns k+1..k+mc equal
+                    const unsigned long long need =
+                        P.mc == 0 ? 0ull : (((1ull << P.mc) - 1ull) << (k + 1));
+                    if ((em & need) == need) {
+                        k += P.mc + 1;
+                        if (k >= 64) {
+                            k = 64;
+                            break;
+                        }
+                        continue;
+                    }
+                    ret = 0;
+                    break;
+                }
+                break;  // the mismatch window crosses the chunk: restart the chunk at k
+            }
+            pos += w.act ? k : 0;
+            col += k;
+            if (ret >= 0) {
+                __syncthreads();
+                return ret;
+            }
+            if (k == 0) {
+                __syncthreads();
+                return 0;
+            }
+        }
+    }
+
+    // is_equal(pos + off, shift, cols), off = 1 for lanes in `shifted`
+    __device__ __forceinline__ bool is_equal_sh(unsigned long long shifted, int shift, int cols) const {
         const int base = pos + (int)((shifted >> w.lane) & 1ull) + shift;
         for (int j = 0; j < cols; j++)
             if (!all_eq(w, ch(base + j))) return false;
         return true;
     }
     // apply_gap :165-174
-    __device__ void apply_gap(unsigned long long shifted, int g) {
+    __device__ __forceinline__ void apply_gap(unsigned long long shifted, int g) {
         const bool s = w.act && ((shifted >> w.lane) & 1ull);
         if (w.act) put(col, s ? (char)ch(pos) : '-');
         pos += s ? 1 : 0;
         col += 1;  // at least one row is shifted (else the column was equal)
         append_cols(g);
     }
-    // try_gap :219-235 with find_all_gaps :176-189 and find_best_gap :191-217
-    __device__ bool try_gap() {
+    // try_gap :219-235 + find_all_gaps :176-189 + find_best_gap :191-217.
+    // Variant k belongs to letter k of the std::set<char> order A < C < G < N < T;
+    // `alive` keeps that order (front() = lowest alive letter).
+    __device__ __forceinline__ bool try_gap() {
         if (is_stop(P.gc)) return false;
-        unsigned long long var[5];
-        int nv = 0;
-        const int c_here = ch(pos);
-        const int c_next = ch(pos + 1);
-        // std::set<char> order: 'A' < 'C' < 'G' < 'N' < 'T'
-        const char order[5] = {'A', 'C', 'G', 'N', 'T'};
+        n_gaps++;
+        const int c_here = ch(pos), c_next = ch(pos + 1);
+        unsigned long long v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+        int alive = 0;
+#pragma unroll
         for (int k = 0; k < 5; k++) {
-            const int c = order[k];
+            const int c = k == 0 ? 'A' : k == 1 ? 'C' : k == 2 ? 'G' : k == 3 ? 'N' : 'T';
             if (!any_lane(w, c_here == c)) continue;
             const bool mt = c_here == c, mn = c_next == c;
             if (any_lane(w, mt == mn)) continue;
-            const unsigned long long shifted = ballot(w.act && mn) & w.rowmask;
-            if (is_equal_sh(shifted, 0, P.gc)) var[nv++] = shifted;
+            const unsigned long long sh = ballot(w.act && mn) & w.rowmask;
+            if (!is_equal_sh(sh, 0, P.gc)) continue;
+            alive |= 1 << k;
+            if (k == 0) v0 = sh;
+            else if (k == 1) v1 = sh;
+            else if (k == 2) v2 = sh;
+            else if (k == 3) v3 = sh;
+            else v4 = sh;
         }
-        if (nv == 0) return false;
-        if (nv == 1) {
-            apply_gap(var[0], P.gc);
+        if (!alive) return false;
+        auto var = [&](int k) { return k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : k == 3 ? v3 : v4; };
+        if (__popc(alive) == 1) {
+            apply_gap(var(__ffs(alive) - 1), P.gc);
             return true;
         }
         for (int g = P.gc + 1;; g++) {
-            unsigned long long nx[5];
-            int nn = 0;
-            for (int k = 0; k < nv; k++)  // columns < g-1 are known equal
-                if (is_equal_sh(var[k], g - 1, 1)) nx[nn++] = var[k];
-            if (nn == 0) {
-                apply_gap(var[0], g - 1);
+            int next = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                if ((alive >> k) & 1)
+                    if (is_equal_sh(var(k), g - 1, 1)) next |= 1 << k;  // columns < g-1 known equal
+            if (!next) {
+                apply_gap(var(__ffs(alive) - 1), g - 1);
                 return true;
             }
-            if (nn == 1) {
-                apply_gap(nx[0], g);
+            if (__popc(next) == 1) {
+                apply_gap(var(__ffs(next) - 1), g);
                 return true;
             }
-            for (int k = 0; k < nn; k++) var[k] = nx[k];
-            nv = nn;
+            alive = next;
         }
     }
 
-    // word code of a letter (injective on ATGCN)
     __device__ static __forceinline__ unsigned long long code3(int c) {
         return c == 'A' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : c == 'N' ? 4 : c == 'T' ? 5 : 6;
     }
 
-    // try_aligned :295-308 + find_best_word :246-272.  Returns true and the
-    // per-lane shift (first shift at which the row shows the chosen word).
-    __device__ bool try_aligned(int& my_shift) {
+    // try_aligned :295-308 + find_best_word :246-272.
+    __device__ __forceinline__ bool try_aligned(int& my_shift) {
         const int mt = wave_min(w.act ? v.len - pos : 0x7fffffff);
         const int max_shift = mt - P.ac;
         if (max_shift <= 0) return false;
-        // fresh epoch of the word table
-        S.epoch += 1;
+        n_aligned_calls++;
+        uint32_t ep32 = epoch + 1;
         const uint32_t tcap = 1u << S.tcap_log2;
-        if (S.epoch >= 0xFFFF) {
+        if (ep32 >= 0xFFFF) {  // epoch wrap: clear the table
             for (uint32_t i = w.lane; i < tcap; i += 64) {
                 S.tkeys[i] = 0ull;
                 S.tmask[i] = 0ull;
             }
             __threadfence();
-            S.epoch = 1;
+            ep32 = 1;
         }
-        const unsigned long long ep = (unsigned long long)S.epoch << 48;
+        epoch = ep32;
+        const unsigned long long ep = (unsigned long long)ep32 << 48;
         const unsigned long long wmask = (P.ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * P.ac)) - 1);
         unsigned long long word = 0;
         if (w.act)
             for (int j = 0; j < P.ac - 1; j++) word = (word << 3) | code3(ch(pos + j));
         for (int s = 0; s < max_shift; s++) {
+            n_shifts++;
             if (w.act) word = ((word << 3) | code3(ch(pos + s + P.ac - 1))) & wmask;
-            // group lanes by word
             unsigned long long remaining = w.rowmask, gm = 0;
             int leader = 0;
-            while (remaining) {
+            while (remaining) {  // group lanes by word
                 const int l = __ffsll((long long)remaining) - 1;
                 const unsigned long long wl = shfl64(word, l);
                 const unsigned long long m = ballot(w.act && word == wl) & w.rowmask;
@@ -247,9 +366,8 @@ struct Proc {
                 }
                 remaining &= ~m;
             }
-            // leaders update the table (one lane per distinct word: no mask races)
             bool complete = false;
-            if (w.act && leader == w.lane) {
+            if (w.act && leader == w.lane) {  // one lane per distinct word: no mask races
                 const unsigned long long key = ep | word;
                 uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - S.tcap_log2));
                 unsigned long long newm;
@@ -260,7 +378,7 @@ struct Proc {
                         newm = atomicOr(&S.tmask[slot], gm) | gm;
                         break;
                     }
-                    if ((k & ~((1ull << 48) - 1)) != ep) {  // stale or empty: claim it
+                    if ((k & ~((1ull << 48) - 1)) != ep) {  // stale or empty: claim
                         if (atomicCAS(&S.tkeys[slot], k, key) == k) {
                             atomicExch(&S.tmask[slot], gm);
                             newm = gm;
@@ -277,11 +395,9 @@ struct Proc {
             if (cm) {
                 const int bl = 63 - __clzll((long long)cm);
                 const unsigned long long best = shfl64(word, bl);
-                const unsigned long long g0 = shfl64(gm, 0);
-                if (g0 == w.rowmask) {  // words.size() == 1: every row at this shift
+                if (shfl64(gm, 0) == w.rowmask) {  // words.size() == 1
                     my_shift = s;
                 } else {
-                    // first shift at which this row produced the best word
                     my_shift = -1;
                     if (w.act) {
                         unsigned long long x = 0;
@@ -301,46 +417,49 @@ struct Proc {
         return false;
     }
 
-    // append_end :323-342
-    __device__ void append_end() {
-        int e = v.len - 1;
+    // append_end :323-342 -- the end walk tests 63 end offsets per pass.
+    // Offset t from the row ends: E(t) = column len_i-1-t identical over rows,
+    // V(t) = every pos_i < len_i-1-t; walk while (V&&E)(t) || (V&&E)(t+1).
+    __device__ __forceinline__ void append_end() {
+        int t = 0;
         while (true) {
-            bool c1 = !any_lane(w, !(pos < e)) && all_eq(w, ch(e));
-            if (!c1) {
-                bool c2 = !any_lane(w, !(pos < e - 1)) && all_eq(w, ch(e - 1));
-                if (!c2) break;
+            const int j = w.lane;
+            const char* p0 = shfl_ptr(v.p, 0);
+            const int d0 = __shfl(v.d, 0), q0 = __shfl(pos, 0), l0 = __shfl(v.len, 0);
+            const int cp0 = l0 - 1 - (t + j);
+            const int c0 = cp0 >= 0 ? (unsigned char)p0[(ptrdiff_t)d0 * cp0] : -1;
+            bool E = true, V = q0 < cp0;
+            for (int r = 1; r < w.n; r++) {
+                const char* pr = shfl_ptr(v.p, r);
+                const int dr = __shfl(v.d, r), lr = __shfl(v.len, r), qr = __shfl(pos, r);
+                const int cp = lr - 1 - (t + j);
+                const int c = cp >= 0 ? (unsigned char)pr[(ptrdiff_t)dr * cp] : -2;
+                E &= c == c0;
+                V &= qr < cp;
             }
-            e -= 1;
+            const unsigned long long a = ballot(E && V);
+            const unsigned long long cond = (a | (a >> 1)) | (1ull << 63);  // bit 63 needs the next chunk
+            const int run = ctz_ones(cond);
+            if (run < 63) {
+                t += run;
+                break;
+            }
+            t += 63;
         }
-        int cols = w.act ? e - pos : 0;
-        const int m = wave_max(cols);
-        if (w.act) {
-            for (int j = 0; j < cols; j++) put(col + j, (char)ch(pos + j));
-            for (int j = cols; j < m; j++) put(col + j, '-');
-            pos += cols;
-        }
-        col += m;
+        int cols = w.act ? (v.len - 1 - t) - pos : 0;
+        if (cols < 0) cols = 0;
+        write_tails(cols, wave_max(cols));  // append_chars to end_pos, append_gaps
         append_all();
     }
 
-    // reverse the output columns [c0, c1) of every row in place
-    __device__ void reverse_cols(int c0, int c1) {
-        if (!w.act) return;
-        if (c1 > out.cap) {
-            ovf = true;
-            return;
+    // One step of process_cols (SimilarAligner.cpp:351-368): a columns-mode run,
+    // then one rows-mode step.  Returns 0 = keep stepping, 1 = frame finished,
+    // 2 = descend into a child (sh = this row's shift).
+    __device__ __forceinline__ int step(int& sh) {
+        if (fast_run() == 1) {
+            append_all();  // is_stop(0)
+            return 1;
         }
-        char* r = out.base + (size_t)w.lane * out.cap;
-        for (int a = c0, b = c1 - 1; a < b; a++, b--) {
-            const char t = r[a];
-            r[a] = r[b];
-            r[b] = t;
-        }
-    }
-
-    // One step of process_cols (SimilarAligner.cpp:351-368).  Returns 0 = keep
-    // stepping, 1 = frame finished, 2 = descend into a child (sh = shift).
-    __device__ int step(int& sh) {
         if (is_stop(0)) {
             append_all();
             return 1;
@@ -349,7 +468,7 @@ struct Proc {
             append_cols(1);
             return 0;
         }
-        if (!is_stop(P.mc) && is_equal_sh(0ull, 1, P.mc)) {  // try_mismatch :122-134
+        if (!is_stop(P.mc) && is_equal_sh(0ull, 1, P.mc)) {  // try_mismatch
             append_cols(P.mc + 1);
             return 0;
         }
@@ -366,9 +485,8 @@ struct Proc {
         return 1;
     }
 
-    // process_seqs on view v0 writing from output column col0; returns the
-    // alignment length.  append_aligned's recursion runs on S's stack.
-    __device__ int run(const View& v0, int col0) {
+    // process_seqs on view v0 from output column col0; returns the length.
+    __device__ __forceinline__ int run(const View& v0, int col0) {
         v = v0;
         pos = 0;
         col = col0;
@@ -405,7 +523,6 @@ struct Proc {
             }
             fresh = false;
             if (r == 0) continue;
-            // frame finished
             if (depth == 0) return col - col0;
             depth--;
             const int child_len = v.len;  // = this row's shift in the parent
@@ -416,7 +533,12 @@ struct Proc {
             v.len = l & 0x7fffffff;
             v.d = (l & (int)0x80000000) ? -1 : 1;
             pos = S.st_pos[o];
-            reverse_cols(c0, col);
+            if (col > cap) {
+                ovf = true;
+            } else {
+                __syncthreads();
+                cm_reverse(w, ob, cap, c0, col);
+            }
             pos += w.act ? child_len : 0;
             append_cols(P.ac);
         }

@@ -47,6 +47,7 @@ struct SaArgs {
     unsigned char* scratch;
     int32_t* job_len;
     int32_t* job_status;       // 0 ok, 1 capacity overflow
+    int64_t* job_stats;        // per job: cycles, columns, aligned calls, shifts, gaps, regions, rows
     unsigned int* next_job;
     // per-slot scratch
     unsigned long long* tkeys;
@@ -78,24 +79,27 @@ __device__ int count_equal_cols(const WaveCtx& w, const char* buf, int cap, int 
     return wave_sum(cnt);
 }
 
-__device__ void copy_cols(const WaveCtx& w, const char* src, char* dst, int cap, int s0, int d0,
-                          int len) {
-    if (!w.act) return;
-    const char* a = src + (size_t)w.lane * cap + s0;
-    char* b = dst + (size_t)w.lane * cap + d0;
-    for (int j = 0; j < len; j++) b[j] = a[j];
-}
-
-// gap-filtered, reversed copy of row segment [s0, s1) into C row (view returned)
+// gap-filtered, reversed copy of every row's segment [s0, s1) into C (columns
+// mode, ballot compaction); returns this lane's row as a view
 __device__ View filter_reverse(const WaveCtx& w, const char* src, char* C, int cap, int s0, int s1) {
-    View v{C + (size_t)w.lane * cap, 0, 1};
-    if (!w.act) return v;
-    const char* a = src + (size_t)w.lane * cap;
-    char* c = C + (size_t)w.lane * cap;
-    int k = 0;
-    for (int j = s1 - 1; j >= s0; j--)
-        if (a[j] != '-') c[k++] = a[j];
-    v.len = k;
+    int my_len = 0;
+    for (int r = 0; r < w.n; r++) {
+        const char* a = src + (size_t)r * cap;
+        char* c = C + (size_t)r * cap;
+        int k = 0;
+        for (int base = s1 - 1; base >= s0; base -= 64) {
+            const int idx = base - w.lane;
+            const bool in = idx >= s0;
+            const char x = in ? a[idx] : '-';
+            const bool keep = in && x != '-';
+            const unsigned long long m = ballot(keep);
+            if (keep) c[k + __popcll(m & ((1ull << w.lane) - 1ull))] = x;
+            k += __popcll(m);
+        }
+        if (w.lane == r) my_len = k;
+    }
+    __syncthreads();
+    View v{C + (size_t)w.lane * cap, w.act ? my_len : 0, 1};
     return v;
 }
 
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
     S.tkeys = a.tkeys + slot * tcap;
     S.tmask = a.tmask + slot * tcap;
     S.tcap_log2 = a.tcap_log2;
-    S.epoch = a.slot_epoch[slot];
+    uint32_t epoch = a.slot_epoch[slot];
     const size_t stn = (size_t)a.st_depth_max * 64;
     S.st_p = a.st_p + slot * stn;
     S.st_len = a.st_len + slot * stn;
@@ -245,6 +249,8 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
             }
             continue;
         }
+        const long long t_job = clock64();
+        int st_calls = 0, st_shifts = 0, st_gaps = 0, st_regions = 0, st_fast = 0;
         WaveCtx w;
         w.lane = lane;
         w.n = n;
@@ -273,9 +279,11 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
             L = m;
         } else {
             // 1. process_seqs
-            Proc pr(w, a.P, S, Out{A, cap});
+            // one Proc for every process_seqs call of the job (state is per call)
+            Proc pr(w, a.P, S, A, cap, epoch);
             const int L0 = pr.run(v0, 0);
             ovf = any_lane(w, pr.ovf);
+
             __syncthreads();
             if (!ovf) {
                 // 2. fix_bad_regions
@@ -283,8 +291,9 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                 __syncthreads();
                 int R = make_regions(w, S.good_col, L0, a.P.wf, S.regions);
                 R = reduce_regions(w, S.regions, R, a.P.min_length);
+                st_regions = R;
                 int colB = 0;
-                Proc q(w, a.P, S, Out{B, cap});
+                pr.ob = B;
                 for (int ri = 0; ri < R && !ovf; ri++) {
                     const int4 rg = S.regions[ri];
                     const int len = rg.y - rg.x + 1;
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                         break;
                     }
                     if (rg.z) {
-                        copy_cols(w, A, B, cap, rg.x, colB, len);
+                        cm_copy(w, A, B, cap, rg.x, colB, len);
                         colB += len;
                         continue;
                     }
@@ -301,8 +310,8 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                     for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
                     before = wave_sum(before);
                     const View cv = filter_reverse(w, A, C, cap, rg.x, rg.y + 1);
-                    const int Lc = q.run(cv, colB);
-                    if (any_lane(w, q.ovf)) {
+                    const int Lc = pr.run(cv, colB);
+                    if (any_lane(w, pr.ovf)) {
                         ovf = true;
                         break;
                     }
@@ -310,10 +319,10 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                     const int after = count_equal_cols(w, B, cap, colB, colB + Lc, nullptr);
                     __syncthreads();
                     if (after > before) {
-                        q.reverse_cols(colB, colB + Lc);
+                        cm_reverse(w, B, cap, colB, colB + Lc);
                         colB += Lc;
                     } else {
-                        copy_cols(w, A, B, cap, rg.x, colB, len);
+                        cm_copy(w, A, B, cap, rg.x, colB, len);
                         colB += len;
                     }
                     __syncthreads();
@@ -324,15 +333,19 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                     int prefix = L - a.P.ac;
                     if (prefix < 1) prefix = 1;
                     const View tv = filter_reverse(w, B, C, cap, prefix, L);
-                    Proc t(w, a.P, S, Out{B, cap});
-                    const int Lt = t.run(tv, prefix);
-                    if (any_lane(w, t.ovf)) ovf = true;
+                    const int Lt = pr.run(tv, prefix);
+                    if (any_lane(w, pr.ovf)) ovf = true;
                     else {
-                        t.reverse_cols(prefix, prefix + Lt);
+                        cm_reverse(w, B, cap, prefix, prefix + Lt);
                         L = prefix + Lt;
                     }
                 }
             }
+            st_calls = pr.n_aligned_calls;
+            st_shifts = pr.n_shifts;
+            st_gaps = pr.n_gaps;
+            st_fast = pr.n_fast;
+            epoch = pr.epoch;
         }
         __syncthreads();
         // 4. remove pure-gap columns
@@ -340,10 +353,19 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
         if (lane == 0) {
             a.job_len[j] = ovf ? 0 : L;
             a.job_status[j] = ovf ? 1 : 0;
+            int64_t* js = a.job_stats + (size_t)j * 8;
+            js[0] = clock64() - t_job;
+            js[1] = L;
+            js[2] = st_calls;
+            js[3] = st_shifts;
+            js[4] = st_gaps;
+            js[5] = st_regions;
+            js[6] = n;
+            js[7] = (int64_t)(st_fast);
         }
         __syncthreads();
     }
-    if (lane == 0) a.slot_epoch[slot] = S.epoch;
+    if (lane == 0) a.slot_epoch[slot] = epoch;
 }
 
 struct GatherRow {
@@ -388,6 +410,8 @@ struct npgx_aligner {
     DevBuf<int32_t> d_row_len;
     DevBuf<SaJob> d_jobs;
     DevBuf<int32_t> d_order, d_job_len, d_job_status;
+    DevBuf<int64_t> d_job_stats;
+    std::vector<int64_t> job_stats;
     DevBuf<unsigned int> d_next;
     DevBuf<unsigned char> d_scratch;
     DevBuf<unsigned long long> tkeys, tmask;
@@ -488,6 +512,8 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
     al->d_order.ensure(order.size());
     al->d_job_len.ensure(jobs.size());
     al->d_job_status.ensure(jobs.size());
+    al->d_job_stats.ensure(jobs.size() * 8);
+    al->job_stats.assign(jobs.size() * 8, 0);
     al->d_next.ensure(1);
     NPGX_HIP(hipMemcpyAsync(al->d_rows.p, packed.data(), packed.size(), hipMemcpyHostToDevice, st));
     if (!poff.empty()) {
@@ -555,6 +581,7 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
         A.scratch = al->d_scratch.p;
         A.job_len = al->d_job_len.p;
         A.job_status = al->d_job_status.p;
+        A.job_stats = al->d_job_stats.p;
         A.next_job = al->d_next.p;
         A.tkeys = al->tkeys.p;
         A.tmask = al->tmask.p;
@@ -579,7 +606,12 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
         al->timer.end(ti, st);
         NPGX_HIP(hipMemcpyAsync(jlen.data(), al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipMemcpyAsync(jstat.data(), al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
+        std::vector<int64_t> jst((size_t)n_jobs * 8);
+        NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipStreamSynchronize(st));
+        for (int32_t j : todo)
+            if (jstat[j] == 0)
+                for (int q = 0; q < 8; q++) al->job_stats[(size_t)j * 8 + q] = jst[(size_t)j * 8 + q];
         std::vector<int32_t> again;
         for (int32_t j : todo)
             if (jstat[j] != 0) again.push_back(j);
@@ -703,6 +735,15 @@ int npgx_align_result_copy(const npgx_aligner* a, char* out, int64_t* out_off, i
         if (out && !a->out_off.empty()) memcpy(out, a->out.data(), (size_t)a->out_off.back());
         if (out_off) memcpy(out_off, a->out_off.data(), a->out_off.size() * 8);
         if (job_len) memcpy(job_len, a->job_len.data(), a->job_len.size() * 8);
+    });
+}
+
+int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64_t* n) {
+    return guard([&] {
+        NPGX_REQUIRE(a && n, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(a->has_result, NPGX_ERR_STATE, "no alignment result yet");
+        *n = (int64_t)a->job_stats.size() / 8;
+        if (out) memcpy(out, a->job_stats.data(), (size_t)std::min<int64_t>(cap, *n) * 64);
     });
 }
 

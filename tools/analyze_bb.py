@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Runs DraftPangenome on a synthetic config a few times and prints the stage
+timings and the aligner's per-job cost profile (GPU box diagnostic)."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+
+from npge_amd import _capi, synth
+from npge_amd.anchor_finder import AnchorFinder
+from npge_amd.blockset import BlockSetEngine
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
+_capi.check(_capi.lib().npgx_set_device(0))
+names, seqs = synth.genome_set(cfg)
+ss = _capi.SeqSet(seqs, names)
+eng = BlockSetEngine(ss)
+for rep in range(3):
+    t = time.perf_counter()
+    eng.apply("DraftPangenome", af=AnchorFinder())
+    dt = time.perf_counter() - t
+st = eng.stats()
+print(json.dumps({"config": cfg, "wall_ms": round(dt * 1e3, 2), "stats": st}, default=str))
+js = eng.job_stats()
+cyc, cols, calls, shifts, gaps, regions, rows, slot = js.T
+print("jobs", len(js), "total cycles %.3e" % cyc.sum(), "columns", cols.sum(), "shifts", shifts.sum(),
+      "aligned calls", calls.sum(), "gaps", gaps.sum())
+order = np.argsort(-cyc)
+print("top jobs by cycles (cycles, cols, calls, shifts, gaps, regions, rows):")
+for i in order[:15]:
+    print("  ", cyc[i], cols[i], calls[i], shifts[i], gaps[i], regions[i], rows[i])
+print("cycles per column (median, p90, p99):", np.percentile(cyc / np.maximum(cols, 1), [50, 90, 99]))
+if shifts.sum():
+    m = shifts > 0
+    print("jobs with shifts:", m.sum(), "cycles share:", cyc[m].sum() / cyc.sum())
+    # regression: cycles ~ a*cols + b*shifts
+    A = np.vstack([cols, shifts, gaps, np.ones_like(cols)]).T.astype(float)
+    coef = np.linalg.lstsq(A, cyc.astype(float), rcond=None)[0]
+    print("fit cycles = %.1f*cols + %.1f*shifts + %.1f*gaps + %.1f" % tuple(coef))
+per_slot = np.bincount(slot, weights=cyc)
+print("slot load: max %.3e mean %.3e" % (per_slot.max(), per_slot[per_slot > 0].mean()))

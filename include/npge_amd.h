@@ -155,9 +155,15 @@ int npgx_align_result_copy(const npgx_aligner* a, char* out, int64_t* out_off,
                            int64_t* job_len);
 int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_t cap,
                             int32_t* n);
-/* per job of the last batch, 8 int64: device cycles, alignment columns,
- * try_aligned calls, shifts scanned, try_gap calls, FindLowSimilar regions,
- * non-empty rows, wave slot */
+/* per job of the last batch, NPGX_JOB_STATS int64: 0 device cycles,
+ * 1 alignment columns, 2 try_aligned calls, 3 shifts scanned, 4 try_gap calls,
+ * 5 FindLowSimilar regions, 6 non-empty rows, 7 columns-mode chunks; cycles
+ * of 8 process_seqs, 9 fix_bad_regions, 10 realing_end, 11 remove_gaps; and,
+ * in a library built with NPGX_SA_PROFILE, cycles inside process_seqs of
+ * 12 columns-mode runs, 13 rows-mode equal/mismatch steps, 14 try_gap,
+ * 15 try_aligned, 16 vector word building, 17 vector word compares,
+ * 18 vector chunks, 19 vector calls, 20-23 spare (0 otherwise) */
+#define NPGX_JOB_STATS 24
 int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64_t* n);
 void npgx_aligner_free(npgx_aligner* a);
 
@@ -202,8 +208,13 @@ typedef struct {
     double ms_host;                 /* wall ms of host bookkeeping */
     /* wall ms per stage of the last apply: 0 AnchorFinder, 1 RemoveNonStem +
      * DummyAligner, 2 MoveUnchanged, 3 flank gather, 4 align batch, 5 stitch,
-     * 6 FixEnds, 7 OverlaplessUnion, 8 blockset hash, 9 Filter */
+     * 6 FixEnds, 7 OverlaplessUnion, 8 blockset hash, 9 Filter,
+     * 10 aligner host preparation, 11 aligner kernel wait */
     double ms_stage[12];
+    /* 0 blocks after ExtendLoopFast, 1 blocks passing Filter whole, 2 blocks
+     * sent to goodSlices, 3 blocks after Filter, 4 blocks into OverlaplessUnion
+     * (all iterations), 5 of them rejected, 6 block hashes computed */
+    int64_t counters[8];
 } npgx_bb_stats;
 
 void npgx_bb_default_options(npgx_bb_options* o);
@@ -226,8 +237,8 @@ int npgx_blockset_hash(const npgx_blockset* b, uint64_t* hash);
 int npgx_blockset_stats(const npgx_blockset* b, npgx_bb_stats* out);
 int npgx_blockset_kernel_times(const npgx_blockset* b, npgx_kernel_time* out, int32_t cap,
                                int32_t* n);
-/* aligner per-job statistics of every batch of the last apply (8 int64 per job,
- * layout of npgx_align_job_stats) */
+/* aligner per-job statistics of every batch of the last apply
+ * (NPGX_JOB_STATS int64 per job, layout of npgx_align_job_stats) */
 int npgx_blockset_job_stats(const npgx_blockset* b, int64_t* out, int64_t cap, int64_t* n);
 void npgx_blockset_free(npgx_blockset* b);
 

@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnpge_amd.so")
+# NPGX_PROFILE=1 selects the diagnostic build with aligner cycle counters
+LIB_PATH = os.path.join(_HERE, "libnpge_amd_prof.so" if os.environ.get("NPGX_PROFILE") == "1"
+                        else "libnpge_amd.so")
 
 NPGX_OK = 0
 ERRORS = {-1: "NPGX_ERR_ARG", -2: "NPGX_ERR_HIP", -3: "NPGX_ERR_NODEV", -4: "NPGX_ERR_RANGE",
@@ -64,7 +66,7 @@ def lib():
     if not os.path.exists(LIB_PATH):
         try:
             from . import build as _b
-            _b.build()
+            _b.build(profile=LIB_PATH.endswith("_prof.so"))
         except Exception as e:  # pragma: no cover - surfaced below
             raise ImportError("npge_amd: HIP library %s missing and could not be built: %s"
                               % (LIB_PATH, e))

@@ -25,10 +25,15 @@ class BbStats(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int64), ("aligned_residues", ctypes.c_int64),
                 ("align_jobs", ctypes.c_int64), ("anchor_blocks", ctypes.c_int64),
                 ("stem_blocks", ctypes.c_int64), ("ms_align", ctypes.c_double),
-                ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 12)]
+                ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 12),
+                ("counters", ctypes.c_int64 * 8)]
 
 STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", "align_batch",
-               "stitch", "fix_ends", "overlapless_union", "blockset_hash", "filter"]
+               "stitch", "fix_ends", "overlapless_union", "blockset_hash", "filter",
+               "align_host_prep", "align_kernel_wait"]
+JOB_STATS = 24  # NPGX_JOB_STATS
+COUNTER_NAMES = ["blocks_after_extend", "filter_whole", "filter_slices", "blocks_after_filter",
+                 "ou_in", "ou_rejected", "hashes", "spare"]
 
 
 def _bind(L):
@@ -146,17 +151,18 @@ class BlockSetEngine:
     def stats(self):
         st = BbStats()
         _capi.check(_capi.lib().npgx_blockset_stats(self._h, ctypes.byref(st)))
-        d = {k: getattr(st, k) for k, _ in BbStats._fields_ if k != "ms_stage"}
+        d = {k: getattr(st, k) for k, _ in BbStats._fields_ if k not in ("ms_stage", "counters")}
         d["ms_stage"] = {n: round(st.ms_stage[i], 3) for i, n in enumerate(STAGE_NAMES)}
+        d["counters"] = {n: int(st.counters[i]) for i, n in enumerate(COUNTER_NAMES)}
         return d
 
     def job_stats(self):
-        """(n_jobs, 8) int64: cycles, columns, try_aligned calls, shifts, gaps,
-        regions, rows, slot of every alignment job of the last apply."""
+        """(n_jobs, NPGX_JOB_STATS) int64 per alignment job of the last apply
+        (layout in include/npge_amd.h, npgx_align_job_stats)."""
         L = _capi.lib()
         n = ctypes.c_int64()
         _capi.check(L.npgx_blockset_job_stats(self._h, None, 0, ctypes.byref(n)))
-        out = np.zeros((max(n.value, 1), 8), dtype=np.int64)
+        out = np.zeros((max(n.value, 1), JOB_STATS), dtype=np.int64)
         _capi.check(L.npgx_blockset_job_stats(self._h, _capi.ptr(out), n.value, ctypes.byref(n)))
         return out[:n.value]
 

@@ -10,30 +10,34 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libnpge_amd.so")
+# diagnostic variant with per-phase cycle counters in the aligner kernel
+# (loaded by _capi when NPGX_PROFILE=1)
+LIB_PROF = os.path.join(HERE, "libnpge_amd_prof.so")
 SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip", "block_build.hip"]
 HEADERS = ["common.hpp", "sa_device.hpp", "log_score.inc"]
 ARCH = os.environ.get("NPGX_OFFLOAD_ARCH", "gfx950")
 
 
-def _stale():
-    if not os.path.exists(LIB):
+def _stale(lib=LIB):
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(os.path.dirname(HERE), "include", "npge_amd.h"))
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
-        return LIB
+def build(force=False, verbose=False, profile=False):
+    lib = LIB_PROF if profile else LIB
+    if not force and not _stale(lib):
+        return lib
     objs = []
     procs = []
     for src in [x for x in SOURCES if os.path.exists(os.path.join(CSRC, x))]:
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
+        obj = os.path.join(CSRC, src.replace(".hip", "_prof.o" if profile else ".o"))
         cmd = ["hipcc", "-c", "-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
                "-munsafe-fp-atomics", "-Wno-unused-result", "-I", os.path.join(os.path.dirname(HERE), "include"),
-               "-o", obj, os.path.join(CSRC, src)]
+               "-o", obj, os.path.join(CSRC, src)] + (["-DNPGX_SA_PROFILE=1"] if profile else [])
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
@@ -42,14 +46,14 @@ def build(force=False, verbose=False):
         out, _ = p.communicate()
         if p.returncode != 0:
             raise RuntimeError("hipcc failed on %s:\n%s" % (src, out.decode(errors="replace")))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = ["hipcc", "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv))

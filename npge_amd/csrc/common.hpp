@@ -133,6 +133,20 @@ int current_device_checked();
 // similar_aligner.hip: batched align_seqs (results in the aligner's host buffers)
 void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
                  const int32_t* job_row_start, int32_t n_jobs);
+// device-resident batch: results stay in the aligner's scratch
+struct AlignResult {
+    std::vector<int32_t> len;          // alignment length per job
+    std::vector<int32_t> cap;          // row stride of the job's output
+    std::vector<int32_t> n;            // non-empty rows per job
+    std::vector<const char*> bptr;     // device address of the job's first output row
+    std::vector<int64_t> row_ne;       // batch row -> index among its job's non-empty rows (-1: empty)
+};
+void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, const int32_t* row_len,
+                  const int32_t* job_row_start, int32_t n_jobs, AlignResult& res);
+void aligner_timer_reset(npgx_aligner* al);
+const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al);
+void aligner_host_ms(npgx_aligner* al, double* prep, double* wait);  // read and clear
+hipStream_t aligner_stream(const npgx_aligner* al);
 const char* aligner_result(const npgx_aligner* al, const int64_t** row_off);
 std::string genome_of(const std::string& name);
 

@@ -24,6 +24,14 @@
 
 #include <cstdint>
 
+#ifdef NPGX_SA_PROFILE
+#define SA_T0(x) const long long x = clock64()
+#define SA_ACC(k, x) prof[k] += clock64() - x
+#else
+#define SA_T0(x)
+#define SA_ACC(k, x)
+#endif
+
 namespace npgx {
 namespace sa {
 
@@ -43,6 +51,10 @@ struct Slot {
     unsigned long long* tkeys;  // try_aligned word table: (epoch << 48 | word)
     unsigned long long* tmask;  // row masks
     uint32_t tcap_log2;
+    unsigned long long* lkeys;  // the same table in LDS (tried first)
+    unsigned long long* lmask;
+    uint32_t ltab_log2;
+    unsigned long long* lwords;  // LDS [row][64]: one chunk's words (vector try_aligned)
     const char** st_p;          // append_aligned stack, 64 lanes per level
     int* st_len;
     int* st_pos;
@@ -51,6 +63,8 @@ struct Slot {
     int4* regions;              // FindLowSimilar regions (start, stop, good, weight)
     unsigned char* good_col;
 };
+
+static constexpr int VEC_ROWS = 8;  // try_aligned with lanes = shifts up to this many rows
 
 struct WaveCtx {
     int lane;
@@ -132,6 +146,195 @@ __device__ __forceinline__ void cm_reverse(const WaveCtx& w, char* base, int cap
     __syncthreads();
 }
 
+__device__ __forceinline__ unsigned long long Proc_code3(int c) {
+    return c == 'A' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : c == 'N' ? 4 : c == 'T' ? 5 : 6;
+}
+
+// find_best_word over 64 shifts at once for up to VEC_ROWS rows: lanes are
+// shifts.  Row i's word at shift s is complete when every row k has had it
+// at some shift <= s: within the chunk by a broadcast compare against row
+// k's 64 words, before the chunk through the global word table, which
+// receives each finished chunk's words (row bits, epoch-tagged).  The
+// first shift with a complete word wins; among the rows complete there the
+// highest one names the word (the reference overwrites best_word row by
+// row), and every row's shift is its first sighting of that word.
+struct VecOut {
+    int found, my_shift, shifts;
+    uint32_t epoch;
+#ifdef NPGX_SA_PROFILE
+    long long t_words, t_cmp;
+    int chunks;
+#endif
+};
+
+// (a free function of scalars: the caller's Proc stays in registers)
+__device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, int pos, int lane, int n, int ac,
+                                             int max_shift, unsigned long long* W, unsigned long long* tkeys,
+                                             unsigned long long* tmask, uint32_t tcap_log2, uint32_t epoch) {
+    // the arguments are wave-uniform: make that visible (scalar loop control)
+    n = __builtin_amdgcn_readfirstlane(n);
+    ac = __builtin_amdgcn_readfirstlane(ac);
+    max_shift = __builtin_amdgcn_readfirstlane(max_shift);
+    tcap_log2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)tcap_log2);
+    epoch = (uint32_t)__builtin_amdgcn_readfirstlane((int)epoch);
+    W = (unsigned long long*)shfl_ptr((const char*)W, 0);
+    VecOut out{};
+    out.epoch = epoch;
+    const View v{vp, vlen, vd};
+    const bool act = lane < n;
+    int my_shift = 0;
+    const unsigned long long wmask = (ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * ac)) - 1);
+    const unsigned long long EPM = ~((1ull << 48) - 1);
+    const uint32_t tcap = 1u << tcap_log2;
+    unsigned long long ep = 0;
+    for (int S0 = 0; S0 < max_shift; S0 += 64) {
+        const int s = S0 + lane;
+        const bool valid = s < max_shift;
+        const int last = __builtin_amdgcn_readfirstlane(min(63, max_shift - 1 - S0));
+#ifdef NPGX_SA_PROFILE
+        out.chunks++;
+        const long long tw0 = clock64();
+#endif
+        for (int k = 0; k < n; k++) {
+            const View vk{shfl_ptr(v.p, k), __shfl(v.len, k), __shfl(v.d, k)};
+            const int qk = __shfl(pos, k) + s;
+            unsigned long long x = 0;
+            if (valid)
+                for (int j = 0; j < ac; j++) x = (x << 3) | Proc_code3(vch(vk, qk + j, lane));
+            W[k * 64 + lane] = x & wmask;
+        }
+        __syncthreads();
+#ifdef NPGX_SA_PROFILE
+        out.t_words += clock64() - tw0;
+        const long long tc0 = clock64();
+#endif
+        const unsigned long long vmask = ballot(valid);
+        int f_best = 64, i_best = -1;
+        for (int i = 0; i < n; i++) {
+            const unsigned long long wi = W[i * 64 + lane];
+            unsigned old = 0;  // rows that had wi before this chunk
+            if (S0 > 0 && valid) {
+                const unsigned long long key = ep | wi;
+                uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tcap_log2));
+                while (true) {
+                    const unsigned long long k = tkeys[slot];
+                    if (k == key) {
+                        const unsigned long long m = tmask[slot];
+                        old = (m & EPM) == ep ? (unsigned)(m & 0xFFu) : 0u;
+                        break;
+                    }
+                    if ((k & EPM) != ep) break;
+                    slot = (slot + 1) & (tcap - 1);
+                }
+            }
+            unsigned long long comp = vmask;
+            for (int k = 0; k < n; k++) {
+                if (k == i) continue;
+                unsigned long long found = ballot((old >> k) & 1u);
+                const unsigned long long wk = W[k * 64 + lane];
+                const unsigned lo = (unsigned)wk, hi = (unsigned)(wk >> 32);
+                for (int t = 0; t <= last; t++) {
+                    const unsigned long long x =
+                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)hi, t) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane((int)lo, t);
+                    found |= ballot(wi == x) & (~0ull << t);
+                }
+                comp &= found;
+            }
+            if (comp) {
+                const int f = __ffsll((long long)comp) - 1;
+                if (f <= f_best) {  // ties: the higher row names the word
+                    f_best = f;
+                    i_best = i;
+                }
+            }
+        }
+#ifdef NPGX_SA_PROFILE
+        out.t_cmp += clock64() - tc0;
+#endif
+        if (i_best >= 0) {
+            out.shifts += f_best + 1;
+            const unsigned long long best = W[i_best * 64 + f_best];
+            bool one = true;
+            for (int k = 0; k < n; k++) one &= W[k * 64 + f_best] == best;
+            if (one) {  // words.size() == 1: every row at this shift
+                my_shift = S0 + f_best;
+            } else if (S0 == 0) {
+                for (int k = 0; k < n; k++) {
+                    const unsigned long long m =
+                        ballot(W[k * 64 + lane] == best) & (f_best == 63 ? ~0ull : ((2ull << f_best) - 1));
+                    if (lane == k) my_shift = __ffsll((long long)m) - 1;
+                }
+            } else {  // first sighting may lie in an earlier chunk: scan the row
+                const int sb = S0 + f_best;
+                my_shift = -1;
+                if (act) {
+                    unsigned long long x = 0;
+                    for (int j = 0; j < ac - 1; j++) x = (x << 3) | Proc_code3(vch(v, pos + j, lane));
+                    for (int t = 0; t <= sb; t++) {
+                        x = ((x << 3) | Proc_code3(vch(v, pos + t + ac - 1, lane))) & wmask;
+                        if (x == best) {
+                            my_shift = t;
+                            break;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            out.found = 1;
+            out.my_shift = my_shift;
+            return out;
+        }
+        out.shifts += last + 1;
+        if (S0 + 64 >= max_shift) break;
+        // remember this chunk's words for the next chunks
+        if (S0 == 0) {
+            uint32_t ep32 = out.epoch + 1;
+            if (ep32 >= 0xFFFF) {
+                for (uint32_t i = lane; i < tcap; i += 64) {
+                    tkeys[i] = 0ull;
+                    tmask[i] = 0ull;
+                }
+                __threadfence();
+                ep32 = 1;
+            }
+            out.epoch = ep32;
+            ep = (unsigned long long)ep32 << 48;
+        }
+        for (int k = 0; k < n; k++) {
+            if (!valid) continue;
+            const unsigned long long key = ep | W[k * 64 + lane];
+            uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tcap_log2));
+            while (true) {
+                const unsigned long long kk =
+                    __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (kk == key) break;
+                if ((kk & EPM) != ep) {
+                    if (atomicCAS(&tkeys[slot], kk, key) == kk) break;
+                    continue;
+                }
+                slot = (slot + 1) & (tcap - 1);
+            }
+            const unsigned long long bit = 1ull << k;
+            unsigned long long m = __hip_atomic_load(&tmask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (true) {
+                if ((m & EPM) == ep) {
+                    atomicOr(&tmask[slot], bit);
+                    break;
+                }
+                const unsigned long long prev = atomicCAS(&tmask[slot], m, ep | bit);
+                if (prev == m) break;
+                m = prev;
+            }
+        }
+        __threadfence();
+        __syncthreads();
+    }
+    __syncthreads();
+    return out;
+}
+
+
 // ---------------------------------------------------------------- process_seqs
 struct Proc {
     WaveCtx w;
@@ -143,13 +346,18 @@ struct Proc {
     int pos;         // this lane's cursor
     int col;         // output cursor (all rows equal length between steps)
     bool ovf;
-    uint32_t epoch;  // word-table epoch (carried from one Proc to the next)
+    uint32_t epoch;   // global word-table epoch (carried from one Proc to the next)
+    uint32_t lepoch;  // LDS word-table epoch
     int n_aligned_calls, n_shifts, n_gaps, n_fast;
+#ifdef NPGX_SA_PROFILE
+    long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fast_run, equal/mismatch steps, try_gap, try_aligned,
+                                                   // vector words, vector compares, chunks, calls
+#endif
 
     __device__ __forceinline__ Proc(const WaveCtx& w_, const Params& P_, const Slot& S_, char* ob_, int cap_,
-                                    uint32_t ep)
-        : w(w_), P(P_), S(S_), ob(ob_), cap(cap_), pos(0), col(0), ovf(false), epoch(ep), n_aligned_calls(0),
-          n_shifts(0), n_gaps(0), n_fast(0) {}
+                                    uint32_t ep, uint32_t lep)
+        : w(w_), P(P_), S(S_), ob(ob_), cap(cap_), pos(0), col(0), ovf(false), epoch(ep), lepoch(lep),
+          n_aligned_calls(0), n_shifts(0), n_gaps(0), n_fast(0) {}
 
     __device__ __forceinline__ void put(int c, char x) {
         if (c < cap) ob[(size_t)w.lane * cap + c] = x;
@@ -329,28 +537,55 @@ struct Proc {
         return c == 'A' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : c == 'N' ? 4 : c == 'T' ? 5 : 6;
     }
 
-    // try_aligned :295-308 + find_best_word :246-272.
+    // try_aligned :295-308 + find_best_word :246-272.  The word table lives in
+    // LDS; a call that inserts more than half of its entries is re-run on the
+    // global table (same result, the table only records first sightings).
     __device__ __forceinline__ bool try_aligned(int& my_shift) {
         const int mt = wave_min(w.act ? v.len - pos : 0x7fffffff);
         const int max_shift = mt - P.ac;
         if (max_shift <= 0) return false;
         n_aligned_calls++;
-        uint32_t ep32 = epoch + 1;
-        const uint32_t tcap = 1u << S.tcap_log2;
+        if (w.n <= VEC_ROWS) {
+            const VecOut r = find_word_vec(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, max_shift, S.lwords, S.tkeys,
+                                           S.tmask, S.tcap_log2, epoch);
+            epoch = r.epoch;
+            n_shifts += r.shifts;
+#ifdef NPGX_SA_PROFILE
+            prof[4] += r.t_words;
+            prof[5] += r.t_cmp;
+            prof[6] += r.chunks;
+            prof[7] += 1;
+#endif
+            if (r.found) my_shift = r.my_shift;
+            return r.found != 0;
+        }
+        const int r = find_word(my_shift, max_shift, S.lkeys, S.lmask, S.ltab_log2, lepoch,
+                                1 << (S.ltab_log2 - 1));
+        if (r >= 0) return r == 1;
+        return find_word(my_shift, max_shift, S.tkeys, S.tmask, S.tcap_log2, epoch, 0x7fffffff) == 1;
+    }
+
+    // 1: found (my_shift set), 0: no shift works, -1: more than `limit` inserts
+    __device__ __forceinline__ int find_word(int& my_shift, int max_shift, unsigned long long* tkeys,
+                                             unsigned long long* tmask, uint32_t tlog, uint32_t& ep_ref,
+                                             int limit) {
+        uint32_t ep32 = ep_ref + 1;
+        const uint32_t tcap = 1u << tlog;
         if (ep32 >= 0xFFFF) {  // epoch wrap: clear the table
             for (uint32_t i = w.lane; i < tcap; i += 64) {
-                S.tkeys[i] = 0ull;
-                S.tmask[i] = 0ull;
+                tkeys[i] = 0ull;
+                tmask[i] = 0ull;
             }
             __threadfence();
             ep32 = 1;
         }
-        epoch = ep32;
+        ep_ref = ep32;
         const unsigned long long ep = (unsigned long long)ep32 << 48;
         const unsigned long long wmask = (P.ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * P.ac)) - 1);
         unsigned long long word = 0;
         if (w.act)
             for (int j = 0; j < P.ac - 1; j++) word = (word << 3) | code3(ch(pos + j));
+        int inserted = 0;
         for (int s = 0; s < max_shift; s++) {
             n_shifts++;
             if (w.act) word = ((word << 3) | code3(ch(pos + s + P.ac - 1))) & wmask;
@@ -366,22 +601,23 @@ struct Proc {
                 }
                 remaining &= ~m;
             }
-            bool complete = false;
+            bool complete = false, claimed = false;
             if (w.act && leader == w.lane) {  // one lane per distinct word: no mask races
                 const unsigned long long key = ep | word;
-                uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - S.tcap_log2));
+                uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tlog));
                 unsigned long long newm;
                 while (true) {
                     const unsigned long long k =
-                        __hip_atomic_load(&S.tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (k == key) {
-                        newm = atomicOr(&S.tmask[slot], gm) | gm;
+                        newm = atomicOr(&tmask[slot], gm) | gm;
                         break;
                     }
                     if ((k & ~((1ull << 48) - 1)) != ep) {  // stale or empty: claim
-                        if (atomicCAS(&S.tkeys[slot], k, key) == k) {
-                            atomicExch(&S.tmask[slot], gm);
+                        if (atomicCAS(&tkeys[slot], k, key) == k) {
+                            atomicExch(&tmask[slot], gm);
                             newm = gm;
+                            claimed = true;
                             break;
                         }
                         continue;
@@ -390,6 +626,7 @@ struct Proc {
                 }
                 complete = (newm == w.rowmask);
             }
+            inserted += __popcll(ballot(claimed));
             const bool comp_i = __shfl(complete ? 1 : 0, leader) != 0;
             const unsigned long long cm = ballot(w.act && comp_i) & w.rowmask;
             if (cm) {
@@ -411,10 +648,11 @@ struct Proc {
                         }
                     }
                 }
-                return true;
+                return 1;
             }
+            if (inserted > limit) return -1;
         }
-        return false;
+        return 0;
     }
 
     // append_end :323-342 -- the end walk tests 63 end offsets per pass.
@@ -456,7 +694,10 @@ struct Proc {
     // then one rows-mode step.  Returns 0 = keep stepping, 1 = frame finished,
     // 2 = descend into a child (sh = this row's shift).
     __device__ __forceinline__ int step(int& sh) {
-        if (fast_run() == 1) {
+        SA_T0(t0);
+        const int fr = fast_run();
+        SA_ACC(0, t0);
+        if (fr == 1) {
             append_all();  // is_stop(0)
             return 1;
         }
@@ -464,17 +705,27 @@ struct Proc {
             append_all();
             return 1;
         }
+        SA_T0(t1);
         if (all_eq(w, ch(pos))) {
             append_cols(1);
+            SA_ACC(1, t1);
             return 0;
         }
         if (!is_stop(P.mc) && is_equal_sh(0ull, 1, P.mc)) {  // try_mismatch
             append_cols(P.mc + 1);
+            SA_ACC(1, t1);
             return 0;
         }
-        if (try_gap()) return 0;
+        SA_ACC(1, t1);
+        SA_T0(t2);
+        const bool gap = try_gap();
+        SA_ACC(2, t2);
+        if (gap) return 0;
         sh = 0;
-        if (try_aligned(sh)) {
+        SA_T0(t3);
+        const bool al = try_aligned(sh);
+        SA_ACC(3, t3);
+        if (al) {
             if (!any_lane(w, sh > 0)) {  // every prefix empty: the child adds nothing
                 append_cols(P.ac);
                 return 0;

@@ -18,6 +18,7 @@
 // row lengths (every column holds a letter); a job first gets a tighter
 // capacity and is re-run at the full bound if it overflows.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -28,6 +29,8 @@
 namespace npgx {
 
 using namespace sa;
+
+static const int64_t LDS_PER_CU = 160 * 1024;  // gfx950: a workgroup may use all of it
 
 struct SaJob {
     int64_t row0;       // first non-empty row (index into row_off / row_len)
@@ -62,6 +65,8 @@ struct SaArgs {
     int4* regions;
     unsigned char* good_col;
     int32_t slot_cols;         // regions / good_col entries per slot
+    int32_t stage_bytes;       // LDS bytes for a job's rows (after the word table)
+    uint32_t ltab_log2;        // LDS word-table entries (log2)
     Params P;
 };
 
@@ -79,13 +84,14 @@ __device__ int count_equal_cols(const WaveCtx& w, const char* buf, int cap, int 
     return wave_sum(cnt);
 }
 
-// gap-filtered, reversed copy of every row's segment [s0, s1) into C (columns
-// mode, ballot compaction); returns this lane's row as a view
-__device__ View filter_reverse(const WaveCtx& w, const char* src, char* C, int cap, int s0, int s1) {
+// gap-filtered, reversed copy of every row's segment [s0, s1) into C (row r
+// at C + r*cstride; columns mode, ballot compaction); returns this lane's row
+// as a view
+__device__ View filter_reverse(const WaveCtx& w, const char* src, int cap, char* C, int cstride, int s0, int s1) {
     int my_len = 0;
     for (int r = 0; r < w.n; r++) {
         const char* a = src + (size_t)r * cap;
-        char* c = C + (size_t)r * cap;
+        char* c = C + (size_t)r * cstride;
         int k = 0;
         for (int base = s1 - 1; base >= s0; base -= 64) {
             const int idx = base - w.lane;
@@ -99,8 +105,16 @@ __device__ View filter_reverse(const WaveCtx& w, const char* src, char* C, int c
         if (w.lane == r) my_len = k;
     }
     __syncthreads();
-    View v{C + (size_t)w.lane * cap, w.act ? my_len : 0, 1};
+    View v{C + (size_t)w.lane * cstride, w.act ? my_len : 0, 1};
     return v;
+}
+
+// segment [s0, s1) of every row, gap-filtered and reversed, into LDS when it fits
+__device__ View stage_segment(const WaveCtx& w, const char* src, int cap, char* C, char* stage, int stage_bytes,
+                              int s0, int s1) {
+    const int len = s1 - s0;
+    if ((int64_t)w.n * len <= stage_bytes) return filter_reverse(w, src, cap, stage, len, s0, s1);
+    return filter_reverse(w, src, cap, C, cap, s0, s1);
 }
 
 // FindLowSimilar::make_regions (:62-80) from good_col[0..L)
@@ -216,9 +230,19 @@ __device__ int remove_pure_gap_cols(const WaveCtx& w, char* buf, int cap, int L)
     return dest;
 }
 
-__global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_jobs(SaArgs a) {
+    extern __shared__ unsigned long long lds_u64[];
     const int lane = threadIdx.x;
     Slot S;
+    const uint32_t ltab = 1u << a.ltab_log2;
+    S.lkeys = lds_u64;
+    S.lmask = lds_u64 + ltab;
+    S.ltab_log2 = a.ltab_log2;
+    S.lwords = lds_u64 + 2 * ltab;
+    for (uint32_t i = lane; i < ltab; i += 64) lds_u64[i] = 0ull;
+    __syncthreads();
+    char* stage = (char*)(lds_u64 + 2 * ltab + 64 * VEC_ROWS);
+    uint32_t lepoch = 0;
     const size_t slot = blockIdx.x;
     const size_t tcap = (size_t)1 << a.tcap_log2;
     S.tkeys = a.tkeys + slot * tcap;
@@ -250,6 +274,7 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
             continue;
         }
         const long long t_job = clock64();
+        long long t_ph[3] = {0, 0, 0}, st_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int st_calls = 0, st_shifts = 0, st_gaps = 0, st_regions = 0, st_fast = 0;
         WaveCtx w;
         w.lane = lane;
@@ -264,6 +289,37 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
         if (w.act) {
             v0.p = a.rows + a.row_off[job.row0 + lane];
             v0.len = a.row_len[job.row0 + lane];
+        }
+        if (a.aligner_type == 0) {
+            // the rows into LDS when they fit: every char(q) of the greedy walk
+            // is then an LDS read instead of a global one
+            int off = 0, tot = 0;
+            for (int r = 0; r < n; r++) {
+                const int lr = __shfl(v0.len, r);
+                if (lane == r) off = tot;
+                tot += lr;
+            }
+            if (tot <= a.stage_bytes) {
+                for (int r = 0; r < n; r++) {
+                    const char* src = shfl_ptr(v0.p, r);
+                    const int lr = __shfl(v0.len, r), o = __shfl(off, r);
+                    for (int base = 0; base < lr; base += 64 * 8) {
+                        char x[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            const int q = base + u * 64 + lane;
+                            x[u] = q < lr ? src[q] : 0;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            const int q = base + u * 64 + lane;
+                            if (q < lr) stage[o + q] = x[u];
+                        }
+                    }
+                }
+                __syncthreads();
+                if (w.act) v0.p = stage + off;
+            }
         }
         bool ovf = false;
         int L = 0;
@@ -280,9 +336,12 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
         } else {
             // 1. process_seqs
             // one Proc for every process_seqs call of the job (state is per call)
-            Proc pr(w, a.P, S, A, cap, epoch);
+            Proc pr(w, a.P, S, A, cap, epoch, lepoch);
+            long long t0 = clock64();
             const int L0 = pr.run(v0, 0);
             ovf = any_lane(w, pr.ovf);
+            t_ph[0] = clock64() - t0;
+            t0 = clock64();
 
             __syncthreads();
             if (!ovf) {
@@ -309,7 +368,7 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                     int before = 0;
                     for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
                     before = wave_sum(before);
-                    const View cv = filter_reverse(w, A, C, cap, rg.x, rg.y + 1);
+                    const View cv = stage_segment(w, A, cap, C, stage, a.stage_bytes, rg.x, rg.y + 1);
                     const int Lc = pr.run(cv, colB);
                     if (any_lane(w, pr.ovf)) {
                         ovf = true;
@@ -328,11 +387,13 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                     __syncthreads();
                 }
                 // 3. realing_end
+                t_ph[1] = clock64() - t0;
+                t0 = clock64();
                 L = colB;
                 if (!ovf && L >= 2) {
                     int prefix = L - a.P.ac;
                     if (prefix < 1) prefix = 1;
-                    const View tv = filter_reverse(w, B, C, cap, prefix, L);
+                    const View tv = stage_segment(w, B, cap, C, stage, a.stage_bytes, prefix, L);
                     const int Lt = pr.run(tv, prefix);
                     if (any_lane(w, pr.ovf)) ovf = true;
                     else {
@@ -340,20 +401,26 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
                         L = prefix + Lt;
                     }
                 }
+                t_ph[2] = clock64() - t0;
             }
+#ifdef NPGX_SA_PROFILE
+            for (int q = 0; q < 8; q++) st_prof[q] = pr.prof[q];
+#endif
             st_calls = pr.n_aligned_calls;
             st_shifts = pr.n_shifts;
             st_gaps = pr.n_gaps;
             st_fast = pr.n_fast;
             epoch = pr.epoch;
+            lepoch = pr.lepoch;
         }
         __syncthreads();
         // 4. remove pure-gap columns
+        const long long t_rg = clock64();
         if (!ovf) L = remove_pure_gap_cols(w, B, cap, L);
         if (lane == 0) {
             a.job_len[j] = ovf ? 0 : L;
             a.job_status[j] = ovf ? 1 : 0;
-            int64_t* js = a.job_stats + (size_t)j * 8;
+            int64_t* js = a.job_stats + (size_t)j * NPGX_JOB_STATS;
             js[0] = clock64() - t_job;
             js[1] = L;
             js[2] = st_calls;
@@ -362,6 +429,12 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
             js[5] = st_regions;
             js[6] = n;
             js[7] = (int64_t)(st_fast);
+            js[8] = t_ph[0];
+            js[9] = t_ph[1];
+            js[10] = t_ph[2];
+            js[11] = clock64() - t_rg;
+            for (int q = 0; q < 8; q++) js[12 + q] = st_prof[q];
+            for (int q = 20; q < NPGX_JOB_STATS; q++) js[q] = 0;
         }
         __syncthreads();
     }
@@ -370,20 +443,20 @@ __global__ __launch_bounds__(64) void k_align_jobs(SaArgs a) {
 
 struct GatherRow {
     int64_t out_off;    // output byte offset
-    int64_t src;        // scratch byte offset of the aligned row (-1: empty row)
+    int64_t src;        // device address of the aligned row (0: empty row -> gaps)
     int32_t len;        // job alignment length
     int32_t pad;
 };
 
-__global__ void k_gather_rows(const GatherRow* rows, int64_t n, const unsigned char* scratch, char* out) {
+__global__ void k_gather_rows(const GatherRow* rows, int64_t n, char* out) {
     const int64_t r = blockIdx.x;
     if (r >= n) return;
     const GatherRow g = rows[r];
     char* d = out + g.out_off;
-    if (g.src < 0) {
+    if (g.src == 0) {
         for (int c = threadIdx.x; c < g.len; c += blockDim.x) d[c] = '-';
     } else {
-        const char* s = (const char*)scratch + g.src;
+        const char* s = (const char*)(uintptr_t)g.src;
         for (int c = threadIdx.x; c < g.len; c += blockDim.x) d[c] = s[c];
     }
 }
@@ -413,7 +486,8 @@ struct npgx_aligner {
     DevBuf<int64_t> d_job_stats;
     std::vector<int64_t> job_stats;
     DevBuf<unsigned int> d_next;
-    DevBuf<unsigned char> d_scratch;
+    DevBuf<unsigned char> d_scratch, d_scratch2;
+    double host_ms[2] = {0, 0};  // align_device: host preparation, kernel wait
     DevBuf<unsigned long long> tkeys, tmask;
     DevBuf<uint32_t> slot_epoch;
     size_t slots_alloc = 0, tcap_alloc = 0, tcap_cur = 0;
@@ -433,24 +507,28 @@ struct npgx_aligner {
 
 namespace npgx {
 
-void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
-                        const int32_t* job_row_start, int32_t n_jobs) {
+// Device-resident batch: row r of the batch is d_rows[row_off[r] .. +row_len[r])
+// (host arrays describing device memory).  Results stay on the device: job j's
+// non-empty row k is at res.bptr[j] + k*res.cap[j] for res.len[j] columns.
+void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, const int32_t* row_len,
+                  const int32_t* job_row_start, int32_t n_jobs, AlignResult& res) {
     NPGX_HIP(hipSetDevice(al->device));
+    auto tp = std::chrono::steady_clock::now();
+    auto ms = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     hipStream_t st = al->stream;
-    al->timer.reset();
-    al->has_result = false;
     const npgx_align_options& o = al->opt;
     NPGX_REQUIRE(n_jobs >= 0, NPGX_ERR_ARG, "n_jobs < 0");
-    const int64_t n_rows = n_jobs ? (int64_t)job_row_start[n_jobs] - job_row_start[0] : 0;
-    // non-empty rows, packed
+    const int64_t r_base = n_jobs ? job_row_start[0] : 0;
+    const int64_t n_rows = n_jobs ? (int64_t)job_row_start[n_jobs] - r_base : 0;
     std::vector<SaJob> jobs(n_jobs);
     std::vector<int64_t> ne_off;
     std::vector<int32_t> ne_len;
-    std::vector<int64_t> row_ne(n_rows > 0 ? n_rows : 1, -1);  // row -> index of non-empty row
+    res.row_ne.assign((size_t)std::max<int64_t>(n_rows, 1), -1);
     std::vector<double> cost(n_jobs);
     int64_t scratch = 0;
     int max_n = 1, max_len = 1, max_cap = 1;
-    const int64_t r_base = n_jobs ? job_row_start[0] : 0;
     for (int32_t j = 0; j < n_jobs; j++) {
         const int64_t r0 = job_row_start[j], r1 = job_row_start[j + 1];
         NPGX_REQUIRE(r1 >= r0, NPGX_ERR_ARG, "job_row_start not monotone");
@@ -460,17 +538,10 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
         int64_t sum = 0;
         int mx = 0;
         for (int64_t r = r0; r < r1; r++) {
-            const int64_t len = row_off[r + 1] - row_off[r];
+            const int64_t len = row_len[r];
             NPGX_REQUIRE(len >= 0 && len < (1ll << 30), NPGX_ERR_RANGE, "row length out of range");
             if (len == 0) continue;
-            if (o.aligner_type == 0) {
-                for (int64_t q = 0; q < len; q++) {
-                    const char c = rows[row_off[r] + q];
-                    NPGX_REQUIRE(c == 'A' || c == 'C' || c == 'G' || c == 'T' || c == 'N', NPGX_ERR_ARG,
-                                 "similar aligner rows must be upper-case ATGCN");
-                }
-            }
-            row_ne[r - r_base] = (int64_t)ne_len.size();
+            res.row_ne[(size_t)(r - r_base)] = (int64_t)ne_len.size() - J.row0;
             ne_off.push_back(row_off[r]);
             ne_len.push_back((int32_t)len);
             n++;
@@ -479,10 +550,10 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
         }
         NPGX_REQUIRE(n <= 64, NPGX_ERR_RANGE, "more than 64 non-empty rows in one alignment");
         J.n = n;
-        // first attempt: 2*max+64 columns (the full bound is the sum of lengths)
+        // first attempt: 2*max+64 columns (the proven bound is the sum of lengths)
         int64_t cap = std::min<int64_t>(sum, 2ll * mx + 64);
         if (o.aligner_type == 1) cap = mx;
-        J.cap = (int32_t)std::max<int64_t>(cap, 1);
+        J.cap = (int32_t)((std::max<int64_t>(cap, 1) + 15) & ~15ll);
         J.scratch = scratch;
         scratch += (3ll * n * J.cap + 255) & ~255ll;
         cost[j] = double(n) * double(sum);
@@ -494,61 +565,53 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
 
-    // device upload of rows (only the non-empty ones, compacted)
-    int64_t bytes = 0;
-    for (size_t i = 0; i < ne_len.size(); i++) bytes += ne_len[i];
-    std::vector<char> packed((size_t)std::max<int64_t>(bytes, 1));
-    std::vector<int64_t> poff(ne_len.size());
-    int64_t b = 0;
-    for (size_t i = 0; i < ne_len.size(); i++) {
-        poff[i] = b;
-        memcpy(packed.data() + b, rows + ne_off[i], (size_t)ne_len[i]);
-        b += ne_len[i];
-    }
-    al->d_rows.ensure(packed.size());
-    al->d_row_off.ensure(poff.size());
+    al->d_row_off.ensure(ne_off.size());
     al->d_row_len.ensure(ne_len.size());
     al->d_jobs.ensure(jobs.size());
     al->d_order.ensure(order.size());
     al->d_job_len.ensure(jobs.size());
     al->d_job_status.ensure(jobs.size());
-    al->d_job_stats.ensure(jobs.size() * 8);
-    al->job_stats.assign(jobs.size() * 8, 0);
+    al->d_job_stats.ensure(jobs.size() * NPGX_JOB_STATS);
+    al->job_stats.assign(jobs.size() * NPGX_JOB_STATS, 0);
     al->d_next.ensure(1);
-    NPGX_HIP(hipMemcpyAsync(al->d_rows.p, packed.data(), packed.size(), hipMemcpyHostToDevice, st));
-    if (!poff.empty()) {
-        NPGX_HIP(hipMemcpyAsync(al->d_row_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, st));
+    if (!ne_off.empty()) {
+        NPGX_HIP(hipMemcpyAsync(al->d_row_off.p, ne_off.data(), ne_off.size() * 8, hipMemcpyHostToDevice, st));
         NPGX_HIP(hipMemcpyAsync(al->d_row_len.p, ne_len.data(), ne_len.size() * 4, hipMemcpyHostToDevice, st));
     }
-    int wf = weight_factor(o.min_identity_x1e4);
+    const int wf = weight_factor(o.min_identity_x1e4);
     Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
 
     std::vector<int32_t> jlen(n_jobs), jstat(n_jobs);
-    std::vector<std::string> row_out((size_t)std::max<int64_t>(n_rows, 0));
-    al->job_len.assign(n_jobs, 0);
+    std::vector<int64_t> jst((size_t)n_jobs * NPGX_JOB_STATS);
+    res.len.assign(n_jobs, 0);
+    res.cap.assign(n_jobs, 0);
+    res.n.assign(n_jobs, 0);
+    res.bptr.assign(n_jobs, nullptr);
+    for (int32_t j = 0; j < n_jobs; j++) res.n[j] = jobs[j].n;
     std::vector<int32_t> todo = order;
     for (int attempt = 0; attempt < 2 && !todo.empty(); attempt++) {
-        if (attempt == 1) {  // re-run overflowed jobs at the proven bound (sum of lengths)
+        DevBuf<unsigned char>& scr = attempt == 0 ? al->d_scratch : al->d_scratch2;
+        if (attempt == 1) {  // re-run overflowed jobs at the proven bound, in a second scratch
             scratch = 0;
             max_cap = 1;
             for (int32_t j : todo) {
                 SaJob& J = jobs[j];
                 int64_t sum = 0;
                 for (int i = 0; i < J.n; i++) sum += ne_len[J.row0 + i];
-                J.cap = (int32_t)std::max<int64_t>(sum, 1);
+                J.cap = (int32_t)((std::max<int64_t>(sum, 1) + 15) & ~15ll);
                 J.scratch = scratch;
                 scratch += (3ll * J.n * J.cap + 255) & ~255ll;
                 max_cap = std::max<int>(max_cap, J.cap);
             }
         }
         const int nj = (int)todo.size();
-        al->d_scratch.ensure((size_t)std::max<int64_t>(scratch, 256));
+        scr.ensure((size_t)std::max<int64_t>(scratch, 256));
         NPGX_HIP(hipMemcpyAsync(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob),
                                 hipMemcpyHostToDevice, st));
         NPGX_HIP(hipMemcpyAsync(al->d_order.p, todo.data(), todo.size() * 4, hipMemcpyHostToDevice, st));
         NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
         // per-slot scratch: word table, append_aligned stack, regions
-        const size_t slots = (size_t)std::max(1, std::min(nj, 2048));
+        const size_t slots = (size_t)std::max(1, std::min(nj, 4096));  // 16 waves on each of 256 CUs
         uint32_t tlog = 10;
         while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
         const size_t tcap = (size_t)1 << tlog;
@@ -558,6 +621,7 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
             al->tmask.ensure(slots * tcap);
             al->slot_epoch.ensure(slots);
             NPGX_HIP(hipMemsetAsync(al->tkeys.p, 0, al->tkeys.cap * 8, st));
+            NPGX_HIP(hipMemsetAsync(al->tmask.p, 0, al->tmask.cap * 8, st));  // epoch-tagged masks (vector search)
             NPGX_HIP(hipMemsetAsync(al->slot_epoch.p, 0, al->slot_epoch.cap * 4, st));
             al->tcap_alloc = std::max(al->tcap_alloc, slots * tcap);
             al->slots_alloc = std::max(al->slots_alloc, slots);
@@ -571,14 +635,14 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
         al->good_col.ensure(slots * (size_t)(max_cap + 1));
 
         SaArgs A;
-        A.rows = al->d_rows.p;
+        A.rows = d_rows;
         A.row_off = al->d_row_off.p;
         A.row_len = al->d_row_len.p;
         A.jobs = al->d_jobs.p;
         A.order = al->d_order.p;
         A.n_jobs = nj;
         A.aligner_type = o.aligner_type;
-        A.scratch = al->d_scratch.p;
+        A.scratch = scr.p;
         A.job_len = al->d_job_len.p;
         A.job_status = al->d_job_status.p;
         A.job_stats = al->d_job_stats.p;
@@ -596,79 +660,137 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
         A.good_col = al->good_col.p;
         A.slot_cols = max_cap + 1;
         A.P = P;
+        // LDS: word table (16 B/entry) + the largest job's rows.  A workgroup may
+        // take all 160 KiB of a CU's LDS; when the batch has more jobs than
+        // workgroups can be resident at that size the stage shrinks, and the
+        // jobs that no longer fit read their rows from global memory.
+        // the LDS word table serves the row-parallel search (more than
+        // VEC_ROWS rows); up to VEC_ROWS rows use the 64-shift vector search
+        A.ltab_log2 = max_n > VEC_ROWS ? 9 : 0;
+        const int table_bytes = (16 << A.ltab_log2) + 64 * VEC_ROWS * 8;  // LDS word table + chunk words
+        int64_t max_rows = 0;
+        for (int32_t j : todo) {
+            int64_t t = 0;
+            for (int i = 0; i < jobs[j].n; i++) t += ne_len[jobs[j].row0 + i];
+            max_rows = std::max(max_rows, t);
+        }
+        const int64_t per_cu = std::min<int64_t>(16, std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
+        const int64_t stage_cap = std::max<int64_t>(0, LDS_PER_CU / per_cu - table_bytes);
+        A.stage_bytes = o.aligner_type == 0 ? (int32_t)std::min<int64_t>((max_rows + 15) & ~15ll, stage_cap & ~15ll) : 0;
+        const size_t lds_bytes = (size_t)table_bytes + (size_t)A.stage_bytes;
+        NPGX_REQUIRE(A.stage_bytes >= 0 && lds_bytes <= (size_t)LDS_PER_CU, NPGX_ERR_STATE, "LDS budget");
         int64_t residues = 0;
         for (int32_t j : todo)
             for (int i = 0; i < jobs[j].n; i++) residues += ne_len[jobs[j].row0 + i];
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
                                     double(residues) * 2.0, residues);
-        hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
         NPGX_HIP(hipMemcpyAsync(jlen.data(), al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipMemcpyAsync(jstat.data(), al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
-        std::vector<int64_t> jst((size_t)n_jobs * 8);
         NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
+        al->host_ms[0] += ms(tp);
+        tp = std::chrono::steady_clock::now();
         NPGX_HIP(hipStreamSynchronize(st));
-        for (int32_t j : todo)
-            if (jstat[j] == 0)
-                for (int q = 0; q < 8; q++) al->job_stats[(size_t)j * 8 + q] = jst[(size_t)j * 8 + q];
+        al->host_ms[1] += ms(tp);
+        tp = std::chrono::steady_clock::now();
         std::vector<int32_t> again;
-        for (int32_t j : todo)
-            if (jstat[j] != 0) again.push_back(j);
+        for (int32_t j : todo) {
+            if (jstat[j] != 0) {
+                again.push_back(j);
+                continue;
+            }
+            for (int q = 0; q < NPGX_JOB_STATS; q++)
+                al->job_stats[(size_t)j * NPGX_JOB_STATS + q] = jst[(size_t)j * NPGX_JOB_STATS + q];
+            res.len[j] = jlen[j];
+            res.cap[j] = jobs[j].cap;
+            // B of the job: rows [n, 2n) of its A|B|C scratch
+            res.bptr[j] = (const char*)(scr.p + jobs[j].scratch + (int64_t)jobs[j].n * jobs[j].cap);
+        }
         if (attempt == 1 && !again.empty())
             throw Error(NPGX_ERR_RANGE, "alignment exceeded the proven column bound");
-        // gather the finished jobs' rows (empty rows become all-gap rows)
-        std::vector<GatherRow> g;
-        std::vector<int64_t> g_row;
-        int64_t tot = 0;
-        for (int32_t j : todo) {
-            if (jstat[j] != 0) continue;
-            al->job_len[j] = jlen[j];
-            for (int64_t r = job_row_start[j]; r < job_row_start[j + 1]; r++) {
-                GatherRow x;
-                x.len = jlen[j];
-                x.pad = 0;
-                x.out_off = tot;
-                const int64_t ne = row_ne[r - r_base];
-                x.src = ne < 0 ? -1
-                               : jobs[j].scratch +
-                                     (int64_t)(jobs[j].n + (ne - jobs[j].row0)) * jobs[j].cap;
-                tot += x.len;
-                g.push_back(x);
-                g_row.push_back(r - r_base);
-            }
-        }
-        if (!g.empty()) {
-            al->d_gather.ensure(g.size());
-            al->d_out.ensure((size_t)std::max<int64_t>(tot, 1));
-            NPGX_HIP(hipMemcpyAsync(al->d_gather.p, g.data(), g.size() * sizeof(GatherRow),
-                                    hipMemcpyHostToDevice, st));
-            size_t tg = al->timer.begin("gather_rows", st, double(tot) * 2.0, tot);
-            hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)g.size()), dim3(64), 0, st, al->d_gather.p,
-                               (int64_t)g.size(), al->d_scratch.p, al->d_out.p);
-            NPGX_HIP(hipGetLastError());
-            al->timer.end(tg, st);
-            std::vector<char> part((size_t)std::max<int64_t>(tot, 1));
-            NPGX_HIP(hipMemcpyAsync(part.data(), al->d_out.p, (size_t)tot, hipMemcpyDeviceToHost, st));
-            NPGX_HIP(hipStreamSynchronize(st));
-            for (size_t i = 0; i < g.size(); i++)
-                row_out[g_row[i]].assign(part.data() + g[i].out_off, (size_t)g[i].len);
-        }
         todo.swap(again);
     }
-    // final layout: rows in input order
-    al->out_off.assign((size_t)std::max<int64_t>(n_rows, 0) + 1, 0);
-    int64_t off = 0;
+    al->host_ms[0] += ms(tp);
+}
+
+void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
+                 const int32_t* job_row_start, int32_t n_jobs) {
+    NPGX_HIP(hipSetDevice(al->device));
+    hipStream_t st = al->stream;
+    al->timer.reset();
+    al->has_result = false;
+    NPGX_REQUIRE(n_jobs >= 0, NPGX_ERR_ARG, "n_jobs < 0");
+    const int64_t r_base = n_jobs ? job_row_start[0] : 0;
+    const int64_t n_rows = n_jobs ? (int64_t)job_row_start[n_jobs] - r_base : 0;
+    // host rows -> device (validated for the similar aligner)
+    const int64_t b0 = n_rows ? row_off[r_base] : 0;
+    const int64_t bytes = n_rows ? row_off[r_base + n_rows] - b0 : 0;
+    std::vector<int64_t> roff((size_t)n_rows + 1);
+    std::vector<int32_t> rlen((size_t)std::max<int64_t>(n_rows, 1));
     for (int64_t r = 0; r < n_rows; r++) {
-        al->out_off[r] = off;
-        off += (int64_t)row_out[r].size();
+        roff[(size_t)r] = row_off[r_base + r] - b0;
+        const int64_t len = row_off[r_base + r + 1] - row_off[r_base + r];
+        NPGX_REQUIRE(len >= 0 && len < (1ll << 30), NPGX_ERR_RANGE, "row length out of range");
+        rlen[(size_t)r] = (int32_t)len;
     }
-    al->out_off[n_rows] = off;
-    al->out.resize((size_t)std::max<int64_t>(off, 1));
-    for (int64_t r = 0; r < n_rows; r++)
-        memcpy(al->out.data() + al->out_off[r], row_out[r].data(), row_out[r].size());
+    if (al->opt.aligner_type == 0)
+        for (int64_t q = 0; q < bytes; q++) {
+            const char c = rows[b0 + q];
+            NPGX_REQUIRE(c == 'A' || c == 'C' || c == 'G' || c == 'T' || c == 'N', NPGX_ERR_ARG,
+                         "similar aligner rows must be upper-case ATGCN");
+        }
+    al->d_rows.ensure((size_t)std::max<int64_t>(bytes, 1));
+    if (bytes) NPGX_HIP(hipMemcpyAsync(al->d_rows.p, rows + b0, (size_t)bytes, hipMemcpyHostToDevice, st));
+    std::vector<int32_t> js((size_t)n_jobs + 1);
+    for (int32_t j = 0; j <= n_jobs; j++) js[(size_t)j] = (int32_t)(job_row_start[j] - r_base);
+    AlignResult res;
+    align_device(al, al->d_rows.p, roff.data(), rlen.data(), js.data(), n_jobs, res);
+    // gather every row (empty rows become all-gap rows), one D2H copy
+    std::vector<GatherRow> g((size_t)n_rows);
+    int64_t tot = 0;
+    al->out_off.assign((size_t)n_rows + 1, 0);
+    al->job_len.assign(n_jobs, 0);
+    for (int32_t j = 0; j < n_jobs; j++) {
+        al->job_len[j] = res.len[j];
+        for (int32_t r = js[j]; r < js[j + 1]; r++) {
+            GatherRow& x = g[(size_t)r];
+            x.len = res.len[j];
+            x.pad = 0;
+            x.out_off = tot;
+            const int64_t k = res.row_ne[(size_t)r];
+            x.src = k < 0 ? 0 : (int64_t)(uintptr_t)(res.bptr[j] + k * res.cap[j]);
+            al->out_off[(size_t)r] = tot;
+            tot += x.len;
+        }
+    }
+    al->out_off[(size_t)n_rows] = tot;
+    al->out.resize((size_t)std::max<int64_t>(tot, 1));
+    if (n_rows && tot) {
+        al->d_gather.ensure(g.size());
+        al->d_out.ensure((size_t)tot);
+        NPGX_HIP(hipMemcpyAsync(al->d_gather.p, g.data(), g.size() * sizeof(GatherRow),
+                                hipMemcpyHostToDevice, st));
+        size_t tg = al->timer.begin("gather_rows", st, double(tot) * 2.0, tot);
+        hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)g.size()), dim3(64), 0, st, al->d_gather.p,
+                           (int64_t)g.size(), al->d_out.p);
+        NPGX_HIP(hipGetLastError());
+        al->timer.end(tg, st);
+        NPGX_HIP(hipMemcpyAsync(al->out.data(), al->d_out.p, (size_t)tot, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipStreamSynchronize(st));
+    }
     al->has_result = true;
 }
+
+void aligner_timer_reset(npgx_aligner* al) { al->timer.reset(); }
+const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al) { return al->job_stats; }
+void aligner_host_ms(npgx_aligner* al, double* prep, double* wait) {
+    *prep = al->host_ms[0];
+    *wait = al->host_ms[1];
+    al->host_ms[0] = al->host_ms[1] = 0;
+}
+hipStream_t aligner_stream(const npgx_aligner* al) { return al->stream; }
 
 const char* aligner_result(const npgx_aligner* al, const int64_t** row_off) {
     *row_off = al->out_off.data();
@@ -707,6 +829,12 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
             delete a;
             throw Error(NPGX_ERR_HIP, "stream creation failed");
         }
+        if (hipFuncSetAttribute((const void*)k_align_jobs, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)LDS_PER_CU) != hipSuccess) {
+            (void)hipStreamDestroy(a->stream);
+            delete a;
+            throw Error(NPGX_ERR_HIP, "cannot enable 160 KiB of LDS for the aligner");
+        }
         *out = a;
     });
 }
@@ -742,8 +870,8 @@ int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64
     return guard([&] {
         NPGX_REQUIRE(a && n, NPGX_ERR_ARG, "null argument");
         NPGX_REQUIRE(a->has_result, NPGX_ERR_STATE, "no alignment result yet");
-        *n = (int64_t)a->job_stats.size() / 8;
-        if (out) memcpy(out, a->job_stats.data(), (size_t)std::min<int64_t>(cap, *n) * 64);
+        *n = (int64_t)a->job_stats.size() / NPGX_JOB_STATS;
+        if (out) memcpy(out, a->job_stats.data(), (size_t)std::min<int64_t>(cap, *n) * NPGX_JOB_STATS * 8);
     });
 }
 

@@ -29,7 +29,8 @@ class BlockBuild:
         return {"anchor_blocks": int(st["anchor_blocks"]), "stem_blocks": int(st["stem_blocks"]),
                 "iterations": int(st["iterations"]), "aligned_residues": int(st["aligned_residues"]),
                 "align_jobs": int(st["align_jobs"]), "ms_align_wall": round(st["ms_align"], 3),
-                "ms_host_bookkeeping": round(st["ms_host"], 3), "ms_stage": st["ms_stage"]}
+                "ms_host_bookkeeping": round(st["ms_host"], 3), "ms_stage": st["ms_stage"],
+                "counters": st["counters"]}
 
     def kernel_times(self):
         """Per-kernel totals of the last step: name -> (ms, bytes, launches)."""

@@ -137,3 +137,27 @@ def test_too_many_rows_rejected():
     from npge_amd import _capi
     with pytest.raises(_capi.NpgxError):
         _aligner().align([["ACGT"] * 65])
+
+
+@pytest.mark.parametrize("cfg", ["tiny", "small"])
+def test_flank_batch(cfg):
+    """Every flank job of the first FragmentsExtender pass of a synthetic set,
+    in ONE batch (thousands of jobs: the launch shrinks its LDS stage), equals
+    the oracle's align_seqs job for job."""
+    from npge_amd import synth
+    from helpers import flank_jobs
+    names, seqs = synth.genome_set(cfg)
+    o = orc.BlockSetOracle(seqs, names)
+    af = orc.AnchorFinder()
+    r = af.run(seqs, names)
+    bs = r["block_start"]
+    blocks = [[(int(r["seq"][i]), int(r["min_pos"][i]), int(r["max_pos"][i]), int(r["ori"][i]), None)
+               for i in range(bs[b], bs[b + 1])] for b in range(len(bs) - 1)]
+    o.set_blocks(blocks)
+    o.apply("RemoveNonStem").apply("DummyAligner")
+    jobs = flank_jobs(o.blocks(), seqs)
+    assert len(jobs) > 100
+    from npge_amd.aligner import BatchAligner
+    gpu = BatchAligner().align(jobs)
+    bad = [j for j, rows in enumerate(jobs) if orc.align(rows, "align_seqs") != gpu[j]]
+    assert not bad, "%d of %d jobs differ (first %d)" % (len(bad), len(jobs), bad[0])

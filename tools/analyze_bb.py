@@ -25,13 +25,23 @@ for rep in range(3):
 st = eng.stats()
 print(json.dumps({"config": cfg, "wall_ms": round(dt * 1e3, 2), "stats": st}, default=str))
 js = eng.job_stats()
-cyc, cols, calls, shifts, gaps, regions, rows, slot = js.T
+os.makedirs("gpurun_out", exist_ok=True)
+np.save("gpurun_out/jobstats_%s%s.npy" % (cfg, "_prof" if os.environ.get("NPGX_PROFILE") == "1" else ""), js)
+cyc, cols, calls, shifts, gaps, regions, rows, fast = js.T[:8]
+ph = js[:, 8:]
 print("jobs", len(js), "total cycles %.3e" % cyc.sum(), "columns", cols.sum(), "shifts", shifts.sum(),
       "aligned calls", calls.sum(), "gaps", gaps.sum())
 order = np.argsort(-cyc)
-print("top jobs by cycles (cycles, cols, calls, shifts, gaps, regions, rows):")
-for i in order[:15]:
-    print("  ", cyc[i], cols[i], calls[i], shifts[i], gaps[i], regions[i], rows[i])
+print("top jobs by cycles (cycles, cols, calls, shifts, gaps, regions, rows, fast runs, cyc/col):")
+for i in order[:25]:
+    print("  ", cyc[i], cols[i], calls[i], shifts[i], gaps[i], regions[i], rows[i], fast[i],
+          round(cyc[i] / max(cols[i], 1), 1))
+names = ["process_seqs", "fix_bad_regions", "realing_end", "remove_gaps", "fast_run", "eq/mismatch",
+         "try_gap", "try_aligned"]
+tot = ph.sum(axis=0)
+print("phase cycles (all jobs):", {n: "%.3e" % t for n, t in zip(names, tot)})
+for i in order[:5]:
+    print("  top job phases:", {n: int(t) for n, t in zip(names, ph[i])})
 print("cycles per column (median, p90, p99):", np.percentile(cyc / np.maximum(cols, 1), [50, 90, 99]))
 if shifts.sum():
     m = shifts > 0
@@ -40,5 +50,8 @@ if shifts.sum():
     A = np.vstack([cols, shifts, gaps, np.ones_like(cols)]).T.astype(float)
     coef = np.linalg.lstsq(A, cyc.astype(float), rcond=None)[0]
     print("fit cycles = %.1f*cols + %.1f*shifts + %.1f*gaps + %.1f" % tuple(coef))
-per_slot = np.bincount(slot, weights=cyc)
-print("slot load: max %.3e mean %.3e" % (per_slot.max(), per_slot[per_slot > 0].mean()))
+big = cols > 20000
+if big.any():
+    A = np.vstack([cols[big], shifts[big], gaps[big], fast[big], np.ones(big.sum())]).T.astype(float)
+    coef = np.linalg.lstsq(A, cyc[big].astype(float), rcond=None)[0]
+    print("long jobs (%d): fit cycles = %.1f*cols + %.1f*shifts + %.1f*gaps + %.1f*fast + %.1f" % ((big.sum(),) + tuple(coef)))

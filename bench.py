@@ -16,7 +16,6 @@ import argparse
 import json
 import os
 import sys
-import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -47,12 +46,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from npge_amd import _capi, synth
-    from npge_amd.anchor_finder import AnchorFinder
+    from npge_amd import _capi, harness, synth
     from npge_amd import pipeline
 
     _capi.check(_capi.lib().npgx_set_device(local_rank))
-    seed = synth.BASE_SEED + 1000 * rank + sum(map(ord, args.config))
+    seed = harness.rank_seed(synth.BASE_SEED, rank, args.config)
     names, seqs = synth.genome_set(args.config, seed=seed)
     bp = synth.total_bp(seqs)
     ss = _capi.SeqSet(seqs, names)          # resident in HBM before timing
@@ -61,26 +59,9 @@ def main():
     def step():
         return job.run()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        info = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    dt = t1 - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    total_bp = bp * world
-    value = total_bp / 1e6 / dt * args.steps
+    dt, info = harness.timed_steps(step, args.steps, args.warmup, dist if world > 1 else None,
+                                   sync=torch.cuda.synchronize, device="cuda")
+    value = harness.throughput(bp, world, args.steps, dt) / 1e6
 
     # dominant kernel of the last step: algorithmic bytes / HIP-event duration
     # (events recorded on the engine's own stream around each launch)
@@ -132,12 +113,15 @@ def main():
 def cpu_baseline(config):
     """The CPU restatement (oracle/, single thread, reference 1-worker semantics)
     timed on this host on the same kind of workload."""
+    import time
     from npge_amd import synth
     from oracle import oracle as orc
-    from npge_amd import pipeline
     names, seqs = synth.genome_set(config)
     bp = synth.total_bp(seqs)
-    t = pipeline.cpu_reference_step(orc, names, seqs)
+    t = time.perf_counter()
+    o = orc.BlockSetOracle(seqs, names, seed=1)
+    o.apply("DraftPangenome")
+    t = time.perf_counter() - t
     return {"value": round(bp / 1e6 / t, 4), "unit": "Mbp/s", "cores": 1, "kind": "port",
             "sample": "%s synthetic set (%d bp), one full step of the same workload, oracle/ "
                       "C++ -O3, 1 thread" % (config, bp), "seconds": round(t, 3)}

@@ -162,7 +162,8 @@ int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_
  * in a library built with NPGX_SA_PROFILE, cycles inside process_seqs of
  * 12 columns-mode runs, 13 rows-mode equal/mismatch steps, 14 try_gap,
  * 15 try_aligned, 16 vector word building, 17 vector word compares,
- * 18 vector chunks, 19 vector calls, 20-23 spare (0 otherwise) */
+ * 18 vector chunks, 19 vector calls, 20 append_end, 21 returns from
+ * append_aligned, 22-23 spare (0 otherwise) */
 #define NPGX_JOB_STATS 24
 int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64_t* n);
 void npgx_aligner_free(npgx_aligner* a);
@@ -209,8 +210,10 @@ typedef struct {
     /* wall ms per stage of the last apply: 0 AnchorFinder, 1 RemoveNonStem +
      * DummyAligner, 2 MoveUnchanged, 3 flank gather, 4 align batch, 5 stitch,
      * 6 FixEnds, 7 OverlaplessUnion, 8 blockset hash, 9 Filter,
-     * 10 aligner host preparation, 11 aligner kernel wait */
-    double ms_stage[12];
+     * 10 aligner host preparation, 11 aligner kernel wait, 12 FixEnds
+     * device part, 13 FixEnds slicing, 14 OverlaplessUnion order,
+     * 15 OverlaplessUnion admission */
+    double ms_stage[16];
     /* 0 blocks after ExtendLoopFast, 1 blocks passing Filter whole, 2 blocks
      * sent to goodSlices, 3 blocks after Filter, 4 blocks into OverlaplessUnion
      * (all iterations), 5 of them rejected, 6 block hashes computed */

@@ -25,12 +25,13 @@ class BbStats(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int64), ("aligned_residues", ctypes.c_int64),
                 ("align_jobs", ctypes.c_int64), ("anchor_blocks", ctypes.c_int64),
                 ("stem_blocks", ctypes.c_int64), ("ms_align", ctypes.c_double),
-                ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 12),
+                ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 16),
                 ("counters", ctypes.c_int64 * 8)]
 
 STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", "align_batch",
                "stitch", "fix_ends", "overlapless_union", "blockset_hash", "filter",
-               "align_host_prep", "align_kernel_wait"]
+               "align_host_prep", "align_kernel_wait", "fix_ends_device", "fix_ends_slice",
+               "ou_order", "ou_admit"]
 JOB_STATS = 24  # NPGX_JOB_STATS
 COUNTER_NAMES = ["blocks_after_extend", "filter_whole", "filter_slices", "blocks_after_filter",
                  "ou_in", "ou_rejected", "hashes", "spare"]

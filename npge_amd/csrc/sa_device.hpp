@@ -54,7 +54,9 @@ struct Slot {
     unsigned long long* lkeys;  // the same table in LDS (tried first)
     unsigned long long* lmask;
     uint32_t ltab_log2;
-    unsigned long long* lwords;  // LDS [row][64]: one chunk's words (vector try_aligned)
+    unsigned long long* lwords;  // LDS [row][64]: one chunk's words (vector try_aligned);
+                                 // more rows: [shift][64] words of the first HIST_SHIFTS shifts
+    int hist_cap;                // > 0: lwords holds HIST_SHIFTS x 64 words
     const char** st_p;          // append_aligned stack, 64 lanes per level
     int* st_len;
     int* st_pos;
@@ -64,7 +66,9 @@ struct Slot {
     unsigned char* good_col;
 };
 
-static constexpr int VEC_ROWS = 8;  // try_aligned with lanes = shifts up to this many rows
+static constexpr int VEC_ROWS = 8;
+typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // LDS-qualified word-table entry
+static constexpr int HIST_SHIFTS = 32;  // words per lane kept for the first-sighting scan  // try_aligned with lanes = shifts up to this many rows
 
 struct WaveCtx {
     int lane;
@@ -350,8 +354,9 @@ struct Proc {
     uint32_t lepoch;  // LDS word-table epoch
     int n_aligned_calls, n_shifts, n_gaps, n_fast;
 #ifdef NPGX_SA_PROFILE
-    long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fast_run, equal/mismatch steps, try_gap, try_aligned,
-                                                   // vector words, vector compares, chunks, calls
+    // fast_run, equal/mismatch steps, try_gap, try_aligned, vector words,
+    // vector compares, chunks, calls, append_end, child return (reverse)
+    long long prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
     __device__ __forceinline__ Proc(const WaveCtx& w_, const Params& P_, const Slot& S_, char* ob_, int cap_,
@@ -559,16 +564,18 @@ struct Proc {
             if (r.found) my_shift = r.my_shift;
             return r.found != 0;
         }
-        const int r = find_word(my_shift, max_shift, S.lkeys, S.lmask, S.ltab_log2, lepoch,
+        const int r = find_word<LdsU64>(my_shift, max_shift, (LdsU64*)S.lkeys, (LdsU64*)S.lmask, S.ltab_log2, lepoch,
                                 1 << (S.ltab_log2 - 1));
         if (r >= 0) return r == 1;
-        return find_word(my_shift, max_shift, S.tkeys, S.tmask, S.tcap_log2, epoch, 0x7fffffff) == 1;
+        return find_word<unsigned long long>(my_shift, max_shift, S.tkeys, S.tmask, S.tcap_log2, epoch,
+                                             0x7fffffff) == 1;
     }
 
     // 1: found (my_shift set), 0: no shift works, -1: more than `limit` inserts
-    __device__ __forceinline__ int find_word(int& my_shift, int max_shift, unsigned long long* tkeys,
-                                             unsigned long long* tmask, uint32_t tlog, uint32_t& ep_ref,
-                                             int limit) {
+    // T = unsigned long long (global table) or LdsU64 (the LDS table: ds_* atomics)
+    template <class T>
+    __device__ __forceinline__ int find_word(int& my_shift, int max_shift, T* tkeys, T* tmask, uint32_t tlog,
+                                             uint32_t& ep_ref, int limit) {
         uint32_t ep32 = ep_ref + 1;
         const uint32_t tcap = 1u << tlog;
         if (ep32 >= 0xFFFF) {  // epoch wrap: clear the table
@@ -582,68 +589,78 @@ struct Proc {
         ep_ref = ep32;
         const unsigned long long ep = (unsigned long long)ep32 << 48;
         const unsigned long long wmask = (P.ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * P.ac)) - 1);
+        // this call's words of the first HIST_SHIFTS shifts, [shift][lane] in LDS:
+        // the first sighting of the chosen word is then a scan of LDS
+        LdsU64* hw = (LdsU64*)S.lwords;
+        const bool keep = S.hist_cap > 0;
         unsigned long long word = 0;
-        if (w.act)
-            for (int j = 0; j < P.ac - 1; j++) word = (word << 3) | code3(ch(pos + j));
+        if (w.act) {
+            int c[15];
+#pragma unroll
+            for (int j = 0; j < 15; j++) c[j] = j < P.ac - 1 ? ch(pos + j) : 0;  // independent loads
+#pragma unroll
+            for (int j = 0; j < 15; j++)
+                if (j < P.ac - 1) word = (word << 3) | code3(c[j]);
+        }
         int inserted = 0;
         for (int s = 0; s < max_shift; s++) {
             n_shifts++;
             if (w.act) word = ((word << 3) | code3(ch(pos + s + P.ac - 1))) & wmask;
-            unsigned long long remaining = w.rowmask, gm = 0;
-            int leader = 0;
-            while (remaining) {  // group lanes by word
-                const int l = __ffsll((long long)remaining) - 1;
-                const unsigned long long wl = shfl64(word, l);
-                const unsigned long long m = ballot(w.act && word == wl) & w.rowmask;
-                if ((m >> w.lane) & 1ull) {
-                    gm = m;
-                    leader = l;
-                }
-                remaining &= ~m;
-            }
-            bool complete = false, claimed = false;
-            if (w.act && leader == w.lane) {  // one lane per distinct word: no mask races
-                const unsigned long long key = ep | word;
-                uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tlog));
-                unsigned long long newm;
+            if (keep && s < HIST_SHIFTS) hw[s * 64 + w.lane] = word;
+            // every row inserts its own word: claim (or find) the key, reset
+            // the row mask of a new key, then OR the row bits in
+            const unsigned long long key = ep | word;
+            uint32_t slot = 0;
+            bool claimed = false;
+            if (w.act) {
+                slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tlog));
                 while (true) {
-                    const unsigned long long k =
-                        __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (k == key) {
-                        newm = atomicOr(&tmask[slot], gm) | gm;
-                        break;
-                    }
+                    unsigned long long k = __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (k == key) break;
                     if ((k & ~((1ull << 48) - 1)) != ep) {  // stale or empty: claim
-                        if (atomicCAS(&tkeys[slot], k, key) == k) {
-                            atomicExch(&tmask[slot], gm);
-                            newm = gm;
+                        if (__hip_atomic_compare_exchange_strong(&tkeys[slot], &k, key, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                             claimed = true;
                             break;
                         }
+                        if (k == key) break;  // another row claimed the same word
                         continue;
                     }
                     slot = (slot + 1) & (tcap - 1);
                 }
-                complete = (newm == w.rowmask);
             }
+            if (claimed) __hip_atomic_store(&tmask[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (w.act)
+                __hip_atomic_fetch_or(&tmask[slot], 1ull << w.lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            const unsigned long long m =
+                w.act ? __hip_atomic_load(&tmask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
             inserted += __popcll(ballot(claimed));
-            const bool comp_i = __shfl(complete ? 1 : 0, leader) != 0;
-            const unsigned long long cm = ballot(w.act && comp_i) & w.rowmask;
+            const unsigned long long cm = ballot(w.act && m == w.rowmask) & w.rowmask;
             if (cm) {
                 const int bl = 63 - __clzll((long long)cm);
                 const unsigned long long best = shfl64(word, bl);
-                if (shfl64(gm, 0) == w.rowmask) {  // words.size() == 1
+                if ((ballot(w.act && word == shfl64(word, 0)) & w.rowmask) == w.rowmask) {  // words.size() == 1
                     my_shift = s;
                 } else {
                     my_shift = -1;
                     if (w.act) {
-                        unsigned long long x = 0;
-                        for (int j = 0; j < P.ac - 1; j++) x = (x << 3) | code3(ch(pos + j));
-                        for (int t = 0; t <= s; t++) {
-                            x = ((x << 3) | code3(ch(pos + t + P.ac - 1))) & wmask;
-                            if (x == best) {
-                                my_shift = t;
-                                break;
+                        if (keep && s < HIST_SHIFTS) {
+                            for (int t = 0; t <= s; t++)
+                                if (hw[t * 64 + w.lane] == best) {
+                                    my_shift = t;
+                                    break;
+                                }
+                        } else {
+                            unsigned long long x = 0;
+                            for (int j = 0; j < P.ac - 1; j++) x = (x << 3) | code3(ch(pos + j));
+                            for (int t = 0; t <= s; t++) {
+                                x = ((x << 3) | code3(ch(pos + t + P.ac - 1))) & wmask;
+                                if (x == best) {
+                                    my_shift = t;
+                                    break;
+                                }
                             }
                         }
                     }
@@ -732,7 +749,9 @@ struct Proc {
             }
             return 2;
         }
+        SA_T0(t4);
         append_end();
+        SA_ACC(8, t4);
         return 1;
     }
 
@@ -775,6 +794,7 @@ struct Proc {
             fresh = false;
             if (r == 0) continue;
             if (depth == 0) return col - col0;
+            SA_T0(t5);
             depth--;
             const int child_len = v.len;  // = this row's shift in the parent
             const size_t o = (size_t)depth * 64 + w.lane;
@@ -792,6 +812,7 @@ struct Proc {
             }
             pos += w.act ? child_len : 0;
             append_cols(P.ac);
+            SA_ACC(9, t5);
         }
     }
 };

@@ -66,6 +66,8 @@ struct SaArgs {
     unsigned char* good_col;
     int32_t slot_cols;         // regions / good_col entries per slot
     int32_t stage_bytes;       // LDS bytes for a job's rows (after the word table)
+    int32_t hist_cap;          // > 0: LDS word history of the row-parallel search
+    int32_t words_bytes;       // LDS bytes of the chunk words / code history
     uint32_t ltab_log2;        // LDS word-table entries (log2)
     Params P;
 };
@@ -239,9 +241,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     S.lmask = lds_u64 + ltab;
     S.ltab_log2 = a.ltab_log2;
     S.lwords = lds_u64 + 2 * ltab;
+    S.hist_cap = a.hist_cap;
     for (uint32_t i = lane; i < ltab; i += 64) lds_u64[i] = 0ull;
     __syncthreads();
-    char* stage = (char*)(lds_u64 + 2 * ltab + 64 * VEC_ROWS);
+    char* stage = (char*)(lds_u64 + 2 * ltab) + a.words_bytes;
     uint32_t lepoch = 0;
     const size_t slot = blockIdx.x;
     const size_t tcap = (size_t)1 << a.tcap_log2;
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             continue;
         }
         const long long t_job = clock64();
-        long long t_ph[3] = {0, 0, 0}, st_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        long long t_ph[3] = {0, 0, 0}, st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         int st_calls = 0, st_shifts = 0, st_gaps = 0, st_regions = 0, st_fast = 0;
         WaveCtx w;
         w.lane = lane;
@@ -404,7 +407,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 t_ph[2] = clock64() - t0;
             }
 #ifdef NPGX_SA_PROFILE
-            for (int q = 0; q < 8; q++) st_prof[q] = pr.prof[q];
+            for (int q = 0; q < 10; q++) st_prof[q] = pr.prof[q];
 #endif
             st_calls = pr.n_aligned_calls;
             st_shifts = pr.n_shifts;
@@ -433,8 +436,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             js[9] = t_ph[1];
             js[10] = t_ph[2];
             js[11] = clock64() - t_rg;
-            for (int q = 0; q < 8; q++) js[12 + q] = st_prof[q];
-            for (int q = 20; q < NPGX_JOB_STATS; q++) js[q] = 0;
+            for (int q = 0; q < 10; q++) js[12 + q] = st_prof[q];
+            for (int q = 22; q < NPGX_JOB_STATS; q++) js[q] = 0;
         }
         __syncthreads();
     }
@@ -664,10 +667,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // take all 160 KiB of a CU's LDS; when the batch has more jobs than
         // workgroups can be resident at that size the stage shrinks, and the
         // jobs that no longer fit read their rows from global memory.
-        // the LDS word table serves the row-parallel search (more than
-        // VEC_ROWS rows); up to VEC_ROWS rows use the 64-shift vector search
-        A.ltab_log2 = max_n > VEC_ROWS ? 9 : 0;
-        const int table_bytes = (16 << A.ltab_log2) + 64 * VEC_ROWS * 8;  // LDS word table + chunk words
+        // LDS per workgroup: the 64-shift chunk words (vector search, up to
+        // VEC_ROWS rows), the word table of the row-parallel search (more rows:
+        // up to half of what is left) and the stage for the job's rows.  The
+        // budget shrinks as more workgroups must be resident per CU.
         int64_t max_rows = 0;
         for (int32_t j : todo) {
             int64_t t = 0;
@@ -675,7 +678,18 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             max_rows = std::max(max_rows, t);
         }
         const int64_t per_cu = std::min<int64_t>(16, std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
-        const int64_t stage_cap = std::max<int64_t>(0, LDS_PER_CU / per_cu - table_bytes);
+        const int64_t budget = LDS_PER_CU / per_cu;
+        // word history of the row-parallel search (HIST_SHIFTS x 64 words) when
+        // the budget allows
+        const int64_t hist_bytes = 64 * HIST_SHIFTS * 8;
+        A.hist_cap = (max_n > VEC_ROWS && hist_bytes * 4 <= budget) ? HIST_SHIFTS : 0;
+        const int64_t words_bytes = std::max<int64_t>(64 * VEC_ROWS * 8, A.hist_cap ? hist_bytes : 0);
+        A.words_bytes = (int32_t)words_bytes;
+        A.ltab_log2 = 0;
+        if (max_n > VEC_ROWS)
+            while (A.ltab_log2 < 12 && (16ll << (A.ltab_log2 + 1)) <= (budget - words_bytes) / 2) A.ltab_log2++;
+        const int table_bytes = (int)((16ll << A.ltab_log2) + words_bytes);
+        const int64_t stage_cap = std::max<int64_t>(0, budget - table_bytes);
         A.stage_bytes = o.aligner_type == 0 ? (int32_t)std::min<int64_t>((max_rows + 15) & ~15ll, stage_cap & ~15ll) : 0;
         const size_t lds_bytes = (size_t)table_bytes + (size_t)A.stage_bytes;
         NPGX_REQUIRE(A.stage_bytes >= 0 && lds_bytes <= (size_t)LDS_PER_CU, NPGX_ERR_STATE, "LDS budget");

@@ -2,8 +2,6 @@
 a device-resident genome set (AnchorFinder -> RemoveNonStem --exact ->
 DummyAligner -> ExtendLoopFast(10) -> Filter, src/algo/lua_lib.lua:1569-1621).
 """
-import time
-
 from .anchor_finder import AnchorFinder
 from .blockset import BlockSetEngine
 
@@ -41,11 +39,3 @@ class BlockBuild:
             a["bytes"] += k["bytes"]
             a["launches"] += 1
         return list(agg.values())
-
-
-def cpu_reference_step(orc, names, seqs, seed=1):
-    """Seconds for the same step on the CPU restatement (1 worker)."""
-    t = time.perf_counter()
-    o = orc.BlockSetOracle(seqs, names, seed=seed)
-    o.apply("DraftPangenome")
-    return time.perf_counter() - t

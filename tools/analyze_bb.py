@@ -18,11 +18,18 @@ _capi.check(_capi.lib().npgx_set_device(0))
 names, seqs = synth.genome_set(cfg)
 ss = _capi.SeqSet(seqs, names)
 eng = BlockSetEngine(ss)
-for rep in range(3):
+best = None
+for rep in range(5):
     t = time.perf_counter()
     eng.apply("DraftPangenome", af=AnchorFinder())
     dt = time.perf_counter() - t
-st = eng.stats()
+    st = eng.stats()
+    if best is None:
+        best = dict(st, ms_stage=dict(st["ms_stage"]))
+    else:
+        for k, v in st["ms_stage"].items():
+            best["ms_stage"][k] = min(best["ms_stage"][k], v)
+st = dict(st, ms_stage_min=best["ms_stage"])
 print(json.dumps({"config": cfg, "wall_ms": round(dt * 1e3, 2), "stats": st}, default=str))
 js = eng.job_stats()
 os.makedirs("gpurun_out", exist_ok=True)

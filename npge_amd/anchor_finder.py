@@ -107,6 +107,11 @@ class AnchorFinder(Processor):
         _capi.check(L.npgx_af_used_hashes(self._h, _capi.ptr(out), n.value, ctypes.byref(n)))
         return out
 
+    def clear_used(self):
+        """Forgets the used hashes (a fresh AnchorFinder without new device buffers)."""
+        if self._h is not None:
+            _capi.check(_capi.lib().npgx_af_clear_used(self._h))
+
     def kernel_times(self):
         return _capi.kernel_times(_capi.lib().npgx_af_kernel_times, self._h)
 

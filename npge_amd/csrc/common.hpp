@@ -4,8 +4,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -129,6 +134,31 @@ struct StageTimer {
 };
 
 int current_device_checked();
+
+// Small persistent host thread pool for the block bookkeeping that is
+// independent per block (hashing).  run(n, f) calls f(i) for i < n on the
+// workers and the calling thread and returns when all are done.
+class HostPool {
+  public:
+    explicit HostPool(int threads);
+    ~HostPool();
+    HostPool(const HostPool&) = delete;
+    HostPool& operator=(const HostPool&) = delete;
+    void run(size_t n, const std::function<void(size_t)>& f);
+    int size() const { return (int)workers_.size() + 1; }
+
+  private:
+    void loop();
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)>* f_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    int active_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 // similar_aligner.hip: batched align_seqs (results in the aligner's host buffers)
 void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,

@@ -101,6 +101,58 @@ __global__ void k_pack(const unsigned char* __restrict__ ascii, const int64_t* _
 
 }  // namespace npgx
 
+namespace npgx {
+
+HostPool::HostPool(int threads) {
+    for (int i = 1; i < threads; i++) workers_.emplace_back([this] { loop(); });
+}
+
+HostPool::~HostPool() {
+    {
+        std::lock_guard<std::mutex> g(m_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+}
+
+void HostPool::loop() {
+    uint64_t seen = 0;
+    while (true) {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        const std::function<void(size_t)>* f = f_;
+        const size_t n = n_;
+        g.unlock();
+        for (size_t i; (i = next_.fetch_add(1)) < n;) (*f)(i);
+        g.lock();
+        if (--active_ == 0) done_.notify_all();
+    }
+}
+
+void HostPool::run(size_t n, const std::function<void(size_t)>& f) {
+    if (workers_.empty() || n < 64) {
+        for (size_t i = 0; i < n; i++) f(i);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> g(m_);
+        f_ = &f;
+        n_ = n;
+        next_ = 0;
+        active_ = (int)workers_.size();
+        gen_++;
+    }
+    cv_.notify_all();
+    for (size_t i; (i = next_.fetch_add(1)) < n;) f(i);
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [&] { return active_ == 0; });
+}
+
+}  // namespace npgx
+
 using namespace npgx;
 
 extern "C" {

@@ -19,6 +19,7 @@
 // capacity and is re-run at the full bound if it overflows.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -505,6 +506,7 @@ struct npgx_aligner {
     std::vector<int64_t> out_off;
     std::vector<int64_t> job_len;
     bool has_result = false;
+    bool want_stats = false;  // per-job statistics copied back (NPGX_JOB_STATS=1)
     StageTimer timer;
 };
 
@@ -575,7 +577,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     al->d_job_len.ensure(jobs.size());
     al->d_job_status.ensure(jobs.size());
     al->d_job_stats.ensure(jobs.size() * NPGX_JOB_STATS);
-    al->job_stats.assign(jobs.size() * NPGX_JOB_STATS, 0);
+    al->job_stats.assign(al->want_stats ? jobs.size() * NPGX_JOB_STATS : 0, 0);
     al->d_next.ensure(1);
     if (!ne_off.empty()) {
         NPGX_HIP(hipMemcpyAsync(al->d_row_off.p, ne_off.data(), ne_off.size() * 8, hipMemcpyHostToDevice, st));
@@ -585,7 +587,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
 
     std::vector<int32_t> jlen(n_jobs), jstat(n_jobs);
-    std::vector<int64_t> jst((size_t)n_jobs * NPGX_JOB_STATS);
+    std::vector<int64_t> jst(al->want_stats ? (size_t)n_jobs * NPGX_JOB_STATS : 0);
     res.len.assign(n_jobs, 0);
     res.cap.assign(n_jobs, 0);
     res.n.assign(n_jobs, 0);
@@ -703,7 +705,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->timer.end(ti, st);
         NPGX_HIP(hipMemcpyAsync(jlen.data(), al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipMemcpyAsync(jstat.data(), al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
+        if (al->want_stats)
+            NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
         al->host_ms[0] += ms(tp);
         tp = std::chrono::steady_clock::now();
         NPGX_HIP(hipStreamSynchronize(st));
@@ -715,8 +718,9 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 again.push_back(j);
                 continue;
             }
-            for (int q = 0; q < NPGX_JOB_STATS; q++)
-                al->job_stats[(size_t)j * NPGX_JOB_STATS + q] = jst[(size_t)j * NPGX_JOB_STATS + q];
+            if (al->want_stats)
+                for (int q = 0; q < NPGX_JOB_STATS; q++)
+                    al->job_stats[(size_t)j * NPGX_JOB_STATS + q] = jst[(size_t)j * NPGX_JOB_STATS + q];
             res.len[j] = jlen[j];
             res.cap[j] = jobs[j].cap;
             // B of the job: rows [n, 2n) of its A|B|C scratch
@@ -839,6 +843,8 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         auto* a = new npgx_aligner;
         a->opt = *o;
         a->device = dev;
+        const char* js = getenv("NPGX_JOB_STATS");
+        a->want_stats = js && js[0] == '1';
         if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
             delete a;
             throw Error(NPGX_ERR_HIP, "stream creation failed");

@@ -13,15 +13,16 @@ class BlockBuild:
         self.ss = seqset
         self.seed = seed
         self.eng = BlockSetEngine(seqset)
-        self.af = None
+        self.af = AnchorFinder()
+        self.af.set_opt_value("bloom-seed", self.seed)
 
     def workload_name(self, config):
         return "%s DraftPangenome: %s" % (config, " -> ".join(STAGES))
 
     def run(self):
-        # a fresh AnchorFinder per step: every step does identical work (no used hashes)
-        self.af = AnchorFinder()
-        self.af.set_opt_value("bloom-seed", self.seed)
+        # one AnchorFinder handle (device buffers kept); its used-hash set is
+        # cleared so that every step does identical work
+        self.af.clear_used()
         self.eng.apply("DraftPangenome", af=self.af)
         st = self.eng.stats()
         return {"anchor_blocks": int(st["anchor_blocks"]), "stem_blocks": int(st["stem_blocks"]),

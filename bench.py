@@ -78,6 +78,9 @@ def main():
     kernels = sorted(({"name": k["name"], "ms": round(k["ms"], 4), "launches": k["launches"]}
                       for k in kts), key=lambda k: -k["ms"])
 
+    if roofline is not None:
+        roofline.update(pmc_traffic(dom["name"], args.config))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample)
@@ -108,6 +111,23 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, config):
+    """HBM traffic per launch of `kernel` from the newest committed PMC summary
+    for this config (profiles/*_<config>_pmc_traffic.json, written by
+    tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
+    of this bench).  PMC counters cannot be read from inside this process."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_%s_pmc_traffic.json" % config.lower())))
+    if not files:
+        return {"traffic": None}
+    doc = json.load(open(files[-1]))
+    for name, v in doc["kernels"].items():
+        if name.split("::")[-1] == "k_" + kernel:
+            return {"traffic": v["traffic_bytes_per_launch"], "traffic_source": os.path.basename(files[-1]),
+                    "traffic_fetch": v["fetch_bytes_per_launch"], "traffic_write": v["write_bytes_per_launch"]}
+    return {"traffic": None}
 
 
 def cpu_baseline(config):

@@ -50,7 +50,7 @@ struct SaArgs {
     int32_t aligner_type;      // 0 similar, 1 dummy
     unsigned char* scratch;
     int32_t* job_len;
-    int32_t* job_status;       // 0 ok, 1 capacity overflow
+    int32_t* job_status;       // 0 ok (rows in B), 2 ok (rows in A), 1 capacity overflow
     int64_t* job_stats;        // per job: cycles, columns, aligned calls, shifts, gaps, regions, rows
     unsigned int* next_job;
     // per-slot scratch
@@ -205,6 +205,80 @@ __device__ int reduce_regions(const WaveCtx& w, int4* reg, int R, int min_length
     return R;
 }
 
+// make_regions + reduce_regions with the regions in registers (lane i holds
+// region i) for alignments of at most 4096 columns and 64 initial regions;
+// good-column masks in registers too (lane c holds columns [64c, 64c+64)).
+// Returns the region count, or -1 when the alignment is outside that range.
+__device__ int regions_in_registers(const WaveCtx& w, const char* A, int cap, int L, int wf, int min_length,
+                                    int4& rg, unsigned long long& gm, int* tmp) {
+    if (L > 64 * 64) return -1;
+    const int lane = w.lane;
+    const int nch = (L + 63) >> 6;
+    gm = 0;
+    for (int ch = 0; ch < nch; ch++) {  // count_equal_cols flags (:416-426)
+        const int c = ch * 64 + lane;
+        bool eq = false;
+        if (c < L) {
+            const char x = A[c];
+            eq = true;
+            for (int r = 1; r < w.n; r++) eq &= A[(size_t)r * cap + c] == x;
+        }
+        const unsigned long long m = ballot(eq);
+        if (lane == ch) gm = m;
+    }
+    const unsigned long long prev = __shfl((long long)gm, lane > 0 ? lane - 1 : 0);
+    const unsigned long long valid =
+        lane < nch - 1 ? ~0ull : lane == nch - 1 ? ((L & 63) ? ((1ull << (L & 63)) - 1) : ~0ull) : 0ull;
+    unsigned long long starts = (gm ^ ((gm << 1) | (lane > 0 ? prev >> 63 : (gm & 1ull)))) & valid;
+    if (lane == 0 && L > 0) starts |= 1ull;  // a region starts at column 0
+    const int cnt = __popcll(starts);
+    int pre = cnt;  // inclusive scan over lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(pre, o);
+        if (lane >= o) pre += t;
+    }
+    const int R = __shfl(pre, 63);
+    if (R > 64) return -1;
+    int idx = pre - cnt;
+    for (unsigned long long m = starts; m; m &= m - 1) tmp[idx++] = lane * 64 + __ffsll((long long)m) - 1;
+    __syncthreads();
+    const int st = lane < R ? tmp[lane] : 0;
+    const int nx = lane + 1 < R ? tmp[lane + 1] : L;
+    __syncthreads();
+    const int good = (int)((((unsigned long long)__shfl((long long)gm, st >> 6)) >> (st & 63)) & 1ull);
+    rg = make_int4(st, nx - 1, good, good ? nx - st : (nx - st) * wf);  // Region::set_weight :48-54
+    int n = R;
+    while (n >= 2) {  // reduce_regions (:121-130)
+        const int wv = lane < n ? rg.w : 0x7fffffff;
+        const int bw = wave_min(wv);
+        if (bw >= min_length) break;
+        const int mi = __ffsll((long long)ballot(lane < n && rg.w == bw)) - 1;  // first minimum
+        int4 nr = make_int4(__shfl(rg.x, mi), __shfl(rg.y, mi), __shfl(rg.z, mi), __shfl(rg.w, mi));
+        const int px = __shfl(rg.x, mi > 0 ? mi - 1 : 0), pw = __shfl(rg.w, mi > 0 ? mi - 1 : 0);
+        const int qy = __shfl(rg.y, mi + 1 < 64 ? mi + 1 : 63), qw = __shfl(rg.w, mi + 1 < 64 ? mi + 1 : 63);
+        int first = mi, last = mi;
+        if (mi > 0) {
+            nr.x = px;
+            nr.w += pw;
+            first = mi - 1;
+        }
+        if (mi < n - 1) {
+            nr.y = qy;
+            nr.w += qw;
+            last = mi + 1;
+        }
+        nr.z = nr.z == 0 ? 1 : 0;
+        const int shiftn = last - first;
+        const int src = lane + shiftn < 64 ? lane + shiftn : 63;
+        const int4 moved = make_int4(__shfl(rg.x, src), __shfl(rg.y, src), __shfl(rg.z, src), __shfl(rg.w, src));
+        if (lane == first) rg = nr;
+        else if (lane > first) rg = moved;
+        n -= shiftn;
+    }
+    return n;
+}
+
 // AbstractAligner.cpp:89-102: drop columns that are '-' in every row
 __device__ int remove_pure_gap_cols(const WaveCtx& w, char* buf, int cap, int L) {
     int dest = 0;
@@ -350,15 +424,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             __syncthreads();
             if (!ovf) {
                 // 2. fix_bad_regions
-                count_equal_cols(w, A, cap, 0, L0, S.good_col);
-                __syncthreads();
-                int R = make_regions(w, S.good_col, L0, a.P.wf, S.regions);
-                R = reduce_regions(w, S.regions, R, a.P.min_length);
+                int4 rreg = make_int4(0, 0, 0, 0);
+                unsigned long long gmask = 0;
+                int R = regions_in_registers(w, A, cap, L0, a.P.wf, a.P.min_length, rreg, gmask, (int*)S.good_col);
+                const bool fast = R >= 0;
+                if (!fast) {
+                    count_equal_cols(w, A, cap, 0, L0, S.good_col);
+                    __syncthreads();
+                    R = make_regions(w, S.good_col, L0, a.P.wf, S.regions);
+                    R = reduce_regions(w, S.regions, R, a.P.min_length);
+                }
                 st_regions = R;
                 int colB = 0;
+                if (fast && R == 1 && __shfl(rreg.z, 0)) {  // one good region: the alignment stays in A
+                    B = A;
+                    colB = L0;
+                    R = 0;
+                }
                 pr.ob = B;
                 for (int ri = 0; ri < R && !ovf; ri++) {
-                    const int4 rg = S.regions[ri];
+                    const int4 rg = fast ? make_int4(__shfl(rreg.x, ri), __shfl(rreg.y, ri), __shfl(rreg.z, ri),
+                                                     __shfl(rreg.w, ri))
+                                         : S.regions[ri];
                     const int len = rg.y - rg.x + 1;
                     if (colB + len > cap) {
                         ovf = true;
@@ -370,7 +457,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         continue;
                     }
                     int before = 0;
-                    for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
+                    if (fast) {
+                        const int lo = lane * 64, hi = lo + 63;
+                        if (lo <= rg.y && hi >= rg.x) {
+                            const int a0 = max(rg.x, lo) - lo, a1 = min(rg.y, hi) - lo;
+                            const unsigned long long m =
+                                (a1 == 63 ? ~0ull : ((1ull << (a1 + 1)) - 1)) & (~0ull << a0);
+                            before = __popcll(gmask & m);
+                        }
+                    } else {
+                        for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
+                    }
                     before = wave_sum(before);
                     const View cv = stage_segment(w, A, cap, C, stage, a.stage_bytes, rg.x, rg.y + 1);
                     const int Lc = pr.run(cv, colB);
@@ -423,7 +520,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (!ovf) L = remove_pure_gap_cols(w, B, cap, L);
         if (lane == 0) {
             a.job_len[j] = ovf ? 0 : L;
-            a.job_status[j] = ovf ? 1 : 0;
+            a.job_status[j] = ovf ? 1 : (B == A ? 2 : 0);  // 2: the rows are in A
             int64_t* js = a.job_stats + (size_t)j * NPGX_JOB_STATS;
             js[0] = clock64() - t_job;
             js[1] = L;
@@ -636,8 +733,9 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->st_len.ensure(slots * depth * 64);
         al->st_pos.ensure(slots * depth * 64);
         al->st_col.ensure(slots * depth);
-        al->regions.ensure(slots * (size_t)(max_cap + 1));
-        al->good_col.ensure(slots * (size_t)(max_cap + 1));
+        const int slot_cols = std::max(max_cap + 1, 256);  // good_col doubles as 64 ints of scratch
+        al->regions.ensure(slots * (size_t)slot_cols);
+        al->good_col.ensure(slots * (size_t)slot_cols);
 
         SaArgs A;
         A.rows = d_rows;
@@ -663,7 +761,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.st_depth_max = depth;
         A.regions = al->regions.p;
         A.good_col = al->good_col.p;
-        A.slot_cols = max_cap + 1;
+        A.slot_cols = slot_cols;
         A.P = P;
         // LDS: word table (16 B/entry) + the largest job's rows.  A workgroup may
         // take all 160 KiB of a CU's LDS; when the batch has more jobs than
@@ -714,7 +812,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         tp = std::chrono::steady_clock::now();
         std::vector<int32_t> again;
         for (int32_t j : todo) {
-            if (jstat[j] != 0) {
+            if (jstat[j] == 1) {
                 again.push_back(j);
                 continue;
             }
@@ -723,8 +821,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                     al->job_stats[(size_t)j * NPGX_JOB_STATS + q] = jst[(size_t)j * NPGX_JOB_STATS + q];
             res.len[j] = jlen[j];
             res.cap[j] = jobs[j].cap;
-            // B of the job: rows [n, 2n) of its A|B|C scratch
-            res.bptr[j] = (const char*)(scr.p + jobs[j].scratch + (int64_t)jobs[j].n * jobs[j].cap);
+            // B of the job (rows [n, 2n) of its A|B|C scratch), or A (status 2)
+            res.bptr[j] = (const char*)(scr.p + jobs[j].scratch + (jstat[j] == 2 ? 0 : (int64_t)jobs[j].n * jobs[j].cap));
         }
         if (attempt == 1 && !again.empty())
             throw Error(NPGX_ERR_RANGE, "alignment exceeded the proven column bound");

@@ -200,12 +200,21 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
         const long long tw0 = clock64();
 #endif
         for (int k = 0; k < n; k++) {
-            const View vk{shfl_ptr(v.p, k), __shfl(v.len, k), __shfl(v.d, k)};
-            const int qk = __shfl(pos, k) + s;
+            // codes of chars q0 .. q0+127 (two coalesced loads), words by shuffles
+            const char* pk = shfl_ptr(v.p, k);
+            const int lk = __shfl(v.len, k), dk = __shfl(v.d, k);
+            const int q0 = __shfl(pos, k) + S0;
+            const int qa = q0 + lane, qb = q0 + 64 + lane;
+            const int ca = qa < lk ? (int)Proc_code3((unsigned char)pk[(ptrdiff_t)dk * qa]) : 6;
+            const int cb = qb < lk ? (int)Proc_code3((unsigned char)pk[(ptrdiff_t)dk * qb]) : 6;
+            const int packed = ca | (cb << 8);
             unsigned long long x = 0;
-            if (valid)
-                for (int j = 0; j < ac; j++) x = (x << 3) | Proc_code3(vch(vk, qk + j, lane));
-            W[k * 64 + lane] = x & wmask;
+            for (int j = 0; j < ac; j++) {
+                const int src = lane + j;
+                const int got = __shfl(packed, src & 63);
+                x = (x << 3) | (unsigned long long)(src < 64 ? (got & 0xFF) : (got >> 8));
+            }
+            W[k * 64 + lane] = valid ? (x & wmask) : 0ull;
         }
         __syncthreads();
 #ifdef NPGX_SA_PROFILE
@@ -237,11 +246,27 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
                 unsigned long long found = ballot((old >> k) & 1u);
                 const unsigned long long wk = W[k * 64 + lane];
                 const unsigned lo = (unsigned)wk, hi = (unsigned)(wk >> 32);
-                for (int t = 0; t <= last; t++) {
-                    const unsigned long long x =
-                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)hi, t) << 32) |
-                        (unsigned)__builtin_amdgcn_readlane((int)lo, t);
-                    found |= ballot(wi == x) & (~0ull << t);
+                if (ac <= 10) {  // 30-bit words: one readlane and a 32-bit compare per shift
+                    const unsigned wi32 = (unsigned)wi;
+                    int t = 0;
+                    for (; t + 3 <= last; t += 4) {
+                        const unsigned x0 = (unsigned)__builtin_amdgcn_readlane((int)lo, t);
+                        const unsigned x1 = (unsigned)__builtin_amdgcn_readlane((int)lo, t + 1);
+                        const unsigned x2 = (unsigned)__builtin_amdgcn_readlane((int)lo, t + 2);
+                        const unsigned x3 = (unsigned)__builtin_amdgcn_readlane((int)lo, t + 3);
+                        found |= (ballot(wi32 == x0) & (~0ull << t)) | (ballot(wi32 == x1) & (~0ull << (t + 1))) |
+                                 (ballot(wi32 == x2) & (~0ull << (t + 2))) |
+                                 (ballot(wi32 == x3) & (~0ull << (t + 3)));
+                    }
+                    for (; t <= last; t++)
+                        found |= ballot(wi32 == (unsigned)__builtin_amdgcn_readlane((int)lo, t)) & (~0ull << t);
+                } else {
+                    for (int t = 0; t <= last; t++) {
+                        const unsigned long long x =
+                            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)hi, t) << 32) |
+                            (unsigned)__builtin_amdgcn_readlane((int)lo, t);
+                        found |= ballot(wi == x) & (~0ull << t);
+                    }
                 }
                 comp &= found;
             }

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -81,6 +82,36 @@ struct DevBuf {
         }
         return p;
     }
+};
+
+// Pinned host staging for async copies (bump allocated; when full, the stream
+// is synchronised so every earlier copy from it has completed).
+struct PinnedArena {
+    char* p = nullptr;
+    size_t cap = 0, used = 0;
+    PinnedArena() = default;
+    PinnedArena(const PinnedArena&) = delete;
+    PinnedArena& operator=(const PinnedArena&) = delete;
+    ~PinnedArena() {
+        if (p) (void)hipHostFree(p);
+    }
+    char* take(size_t n, hipStream_t st) {
+        n = (n + 63) & ~(size_t)63;
+        if (used + n > cap) {
+            NPGX_HIP(hipStreamSynchronize(st));
+            used = 0;
+            if (n > cap) {
+                if (p) (void)hipHostFree(p);
+                p = nullptr;
+                cap = std::max<size_t>(std::max<size_t>(n, 2 * cap), (size_t)1 << 22);
+                NPGX_HIP(hipHostMalloc((void**)&p, cap, hipHostMallocDefault));
+            }
+        }
+        char* r = p + used;
+        used += n;
+        return r;
+    }
+    void reset() { used = 0; }  // only with no copy from it in flight
 };
 
 // Stage timer: pairs of HIP events on one stream.

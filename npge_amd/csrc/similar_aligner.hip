@@ -57,7 +57,8 @@ struct SaArgs {
     unsigned long long* tkeys;
     unsigned long long* tmask;
     uint32_t tcap_log2;
-    uint32_t* slot_epoch;
+    uint32_t* slot_epoch;      // out: highest word-table epoch reached (one word)
+    uint32_t epoch_base;       // every slot's first epoch
     const char** st_p;
     int* st_len;
     int* st_pos;
@@ -326,7 +327,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     S.tkeys = a.tkeys + slot * tcap;
     S.tmask = a.tmask + slot * tcap;
     S.tcap_log2 = a.tcap_log2;
-    uint32_t epoch = a.slot_epoch[slot];
+    uint32_t epoch = a.epoch_base;
     const size_t stn = (size_t)a.st_depth_max * 64;
     S.st_p = a.st_p + slot * stn;
     S.st_len = a.st_len + slot * stn;
@@ -539,7 +540,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
         __syncthreads();
     }
-    if (lane == 0) a.slot_epoch[slot] = epoch;
+    if (lane == 0) atomicMax(a.slot_epoch, epoch);  // the launch's highest epoch
 }
 
 struct GatherRow {
@@ -591,7 +592,8 @@ struct npgx_aligner {
     double host_ms[2] = {0, 0};  // align_device: host preparation, kernel wait
     DevBuf<unsigned long long> tkeys, tmask;
     DevBuf<uint32_t> slot_epoch;
-    size_t slots_alloc = 0, tcap_alloc = 0, tcap_cur = 0;
+    size_t tcap_alloc = 0;
+    uint32_t epoch_base = 1;  // first word-table epoch of the next launch
     DevBuf<const char*> st_p;
     DevBuf<int> st_len, st_pos, st_col;
     DevBuf<int4> regions;
@@ -718,17 +720,20 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
         const size_t tcap = (size_t)1 << tlog;
         const int depth = max_len / std::max(1, o.aligned_check + 1) + 4;
-        if (slots * tcap > al->tcap_alloc || slots > al->slots_alloc || tcap != al->tcap_cur) {
+        // Word tables: epochs only grow from launch to launch (every slot starts
+        // at the last launch's highest epoch + 1), so entries left by earlier
+        // launches never match, whatever the slot layout; the tables are
+        // cleared only when they grow or the 16-bit epochs run out.
+        if (slots * tcap > al->tcap_alloc || al->epoch_base > 0xF000) {
             al->tkeys.ensure(slots * tcap);
             al->tmask.ensure(slots * tcap);
-            al->slot_epoch.ensure(slots);
             NPGX_HIP(hipMemsetAsync(al->tkeys.p, 0, al->tkeys.cap * 8, st));
             NPGX_HIP(hipMemsetAsync(al->tmask.p, 0, al->tmask.cap * 8, st));  // epoch-tagged masks (vector search)
-            NPGX_HIP(hipMemsetAsync(al->slot_epoch.p, 0, al->slot_epoch.cap * 4, st));
             al->tcap_alloc = std::max(al->tcap_alloc, slots * tcap);
-            al->slots_alloc = std::max(al->slots_alloc, slots);
-            al->tcap_cur = tcap;
+            al->epoch_base = 1;
         }
+        al->slot_epoch.ensure(1);
+        NPGX_HIP(hipMemsetAsync(al->slot_epoch.p, 0, 4, st));
         al->st_p.ensure(slots * depth * 64);
         al->st_len.ensure(slots * depth * 64);
         al->st_pos.ensure(slots * depth * 64);
@@ -754,6 +759,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.tmask = al->tmask.p;
         A.tcap_log2 = tlog;
         A.slot_epoch = al->slot_epoch.p;
+        A.epoch_base = al->epoch_base;
         A.st_p = al->st_p.p;
         A.st_len = al->st_len.p;
         A.st_pos = al->st_pos.p;
@@ -803,6 +809,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->timer.end(ti, st);
         NPGX_HIP(hipMemcpyAsync(jlen.data(), al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipMemcpyAsync(jstat.data(), al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
+        uint32_t ep_max = 0;
+        NPGX_HIP(hipMemcpyAsync(&ep_max, al->slot_epoch.p, 4, hipMemcpyDeviceToHost, st));
         if (al->want_stats)
             NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
         al->host_ms[0] += ms(tp);
@@ -810,6 +818,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         NPGX_HIP(hipStreamSynchronize(st));
         al->host_ms[1] += ms(tp);
         tp = std::chrono::steady_clock::now();
+        al->epoch_base = std::max(al->epoch_base, ep_max + 1);
         std::vector<int32_t> again;
         for (int32_t j : todo) {
             if (jstat[j] == 1) {

@@ -117,3 +117,23 @@ def test_filter_and_fix_ends_fixture():
         got = sorted(("%s_%d_%d" % (names[s], mn, mx), row) for b in eng.blocks()
                      for s, mn, mx, ori, row in b)
         assert got == want, proc
+
+
+@pytest.mark.parametrize("case,opts", [("stem", ""), ("stem-exact", " --exact")])
+def test_remove_non_stem_fixture(case, opts):
+    """test-script/stem/1 and stem-exact/1 (RemoveNonStem, RemoveNonStem
+    --exact): the fixtures hold fragments only; the sequences a&1&c, b&1&c,
+    c&1&c (genomes a, b, c) are synthesised long enough for them."""
+    from npge_amd.io import read_blockset
+    d = os.path.join(GOLD, case, "1")
+    src = read_blockset(open(os.path.join(d, "in.fasta")).read())
+    exp = read_blockset(open(os.path.join(d, "out.fasta")).read())
+    names = ["a&1&c", "b&1&c", "c&1&c"]
+    seqs = ["A" * 40] * 3
+    idx = {n: i for i, n in enumerate(names)}
+    blocks = [[(idx[f.seq.name], f.min_pos, f.max_pos, f.ori, None) for f in b.fragments] for b in src.blocks]
+    ss, eng = _engine(seqs, names)
+    eng.set_blocks(blocks).apply("RemoveNonStem" + opts)
+    got = canon([[(s, mn, mx, o) for (s, mn, mx, o, _) in b] for b in eng.blocks()])
+    want = canon([[(idx[f.seq.name], f.min_pos, f.max_pos, f.ori) for f in b.fragments] for b in exp.blocks])
+    assert got == want

@@ -590,6 +590,7 @@ struct npgx_aligner {
     DevBuf<unsigned int> d_next;
     DevBuf<unsigned char> d_scratch, d_scratch2;
     double host_ms[2] = {0, 0};  // align_device: host preparation, kernel wait
+    PinnedArena pinned;          // staging of the batch's host<->device copies
     DevBuf<unsigned long long> tkeys, tmask;
     DevBuf<uint32_t> slot_epoch;
     size_t tcap_alloc = 0;
@@ -665,9 +666,25 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         max_len = std::max(max_len, mx);
         max_cap = std::max<int>(max_cap, J.cap);
     }
+    // heaviest first (rows x residues), by power-of-two cost classes: the order
+    // only balances the load, results do not depend on it
     std::vector<int32_t> order(n_jobs);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    {
+        int cnt[65] = {0};
+        std::vector<uint8_t> cls(n_jobs);
+        for (int32_t j = 0; j < n_jobs; j++) {
+            const uint64_t c = (uint64_t)cost[j];
+            cls[j] = (uint8_t)(c ? 64 - __builtin_clzll(c) : 0);  // 0..64
+            cnt[cls[j]]++;
+        }
+        int at[65];
+        int acc = 0;
+        for (int c = 64; c >= 0; c--) {
+            at[c] = acc;
+            acc += cnt[c];
+        }
+        for (int32_t j = 0; j < n_jobs; j++) order[at[cls[j]]++] = j;
+    }
 
     al->d_row_off.ensure(ne_off.size());
     al->d_row_len.ensure(ne_len.size());
@@ -678,10 +695,14 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     al->d_job_stats.ensure(jobs.size() * NPGX_JOB_STATS);
     al->job_stats.assign(al->want_stats ? jobs.size() * NPGX_JOB_STATS : 0, 0);
     al->d_next.ensure(1);
-    if (!ne_off.empty()) {
-        NPGX_HIP(hipMemcpyAsync(al->d_row_off.p, ne_off.data(), ne_off.size() * 8, hipMemcpyHostToDevice, st));
-        NPGX_HIP(hipMemcpyAsync(al->d_row_len.p, ne_len.data(), ne_len.size() * 4, hipMemcpyHostToDevice, st));
-    }
+    auto put = [&](void* d, const void* h, size_t bytes) {  // through pinned staging
+        if (!bytes) return;
+        char* p = al->pinned.take(bytes, st);
+        memcpy(p, h, bytes);
+        NPGX_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, st));
+    };
+    put(al->d_row_off.p, ne_off.data(), ne_off.size() * 8);
+    put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
     const int wf = weight_factor(o.min_identity_x1e4);
     Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
 
@@ -710,9 +731,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         }
         const int nj = (int)todo.size();
         scr.ensure((size_t)std::max<int64_t>(scratch, 256));
-        NPGX_HIP(hipMemcpyAsync(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob),
-                                hipMemcpyHostToDevice, st));
-        NPGX_HIP(hipMemcpyAsync(al->d_order.p, todo.data(), todo.size() * 4, hipMemcpyHostToDevice, st));
+        put(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob));
+        put(al->d_order.p, todo.data(), todo.size() * 4);
         NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
         // per-slot scratch: word table, append_aligned stack, regions
         const size_t slots = (size_t)std::max(1, std::min(nj, 4096));  // 16 waves on each of 256 CUs
@@ -807,10 +827,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
-        NPGX_HIP(hipMemcpyAsync(jlen.data(), al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipMemcpyAsync(jstat.data(), al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
-        uint32_t ep_max = 0;
-        NPGX_HIP(hipMemcpyAsync(&ep_max, al->slot_epoch.p, 4, hipMemcpyDeviceToHost, st));
+        int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);
+        NPGX_HIP(hipMemcpyAsync(pl, al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipMemcpyAsync(pl + n_jobs, al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipMemcpyAsync(pl + 2 * n_jobs, al->slot_epoch.p, 4, hipMemcpyDeviceToHost, st));
         if (al->want_stats)
             NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
         al->host_ms[0] += ms(tp);
@@ -818,7 +838,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         NPGX_HIP(hipStreamSynchronize(st));
         al->host_ms[1] += ms(tp);
         tp = std::chrono::steady_clock::now();
-        al->epoch_base = std::max(al->epoch_base, ep_max + 1);
+        memcpy(jlen.data(), pl, n_jobs * 4);
+        memcpy(jstat.data(), pl + n_jobs, n_jobs * 4);
+        al->epoch_base = std::max(al->epoch_base, (uint32_t)pl[2 * n_jobs] + 1);
+        al->pinned.reset();
         std::vector<int32_t> again;
         for (int32_t j : todo) {
             if (jstat[j] == 1) {

@@ -163,7 +163,8 @@ int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_
  * 12 columns-mode runs, 13 rows-mode equal/mismatch steps, 14 try_gap,
  * 15 try_aligned, 16 vector word building, 17 vector word compares,
  * 18 vector chunks, 19 vector calls, 20 append_end, 21 returns from
- * append_aligned, 22-23 spare (0 otherwise) */
+ * append_aligned (0 otherwise); 22 cycles of the region search, 23 regions
+ * before merging (alignments over 4096 columns) */
 #define NPGX_JOB_STATS 24
 int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64_t* n);
 void npgx_aligner_free(npgx_aligner* a);

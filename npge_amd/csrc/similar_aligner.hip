@@ -280,6 +280,101 @@ __device__ int regions_in_registers(const WaveCtx& w, const char* A, int cap, in
     return n;
 }
 
+typedef __attribute__((address_space(3))) int LdsInt;
+
+// make_regions (:62-80) + reduce_regions (:121-130) for long alignments, in
+// LDS (the job's row stage, free after process_seqs): regions as arrays with
+// prev/next links; a merge rewrites the surviving region and unlinks the
+// others (no shifting); the minimum is a wave-parallel scan over the array
+// (alive entries keep their order, so the lowest index is the reference's
+// first minimum).  The survivors go to `out` in order; returns their count,
+// or -1 when the LDS area is too small.
+__device__ int regions_in_lds(const WaveCtx& w, const unsigned char* good, int L, int wf, int min_length,
+                              LdsInt* area, int area_bytes, int4* out) {
+    const int lane = w.lane;
+    // count region starts first
+    int R0 = 0;
+    for (int base = 0; base < L; base += 64) {
+        const int j = base + lane;
+        const bool b = j < L && (j == 0 || good[j] != good[j - 1]);
+        R0 += __popcll(ballot(b));
+    }
+    if ((long long)R0 * 24 > area_bytes) return -1;
+    LdsInt *rx = area, *ry = area + R0, *rz = area + 2 * R0, *rw = area + 3 * R0, *nx = area + 4 * R0,
+           *pv = area + 5 * R0;
+    int k = 0;
+    for (int base = 0; base < L; base += 64) {
+        const int j = base + lane;
+        const bool b = j < L && (j == 0 || good[j] != good[j - 1]);
+        const unsigned long long m = ballot(b);
+        if (b) {
+            const int i = k + __popcll(m & ((1ull << lane) - 1ull));
+            rx[i] = j;
+            rz[i] = good[j];
+        }
+        k += __popcll(m);
+    }
+    __syncthreads();
+    for (int i = lane; i < R0; i += 64) {
+        const int stop = i + 1 < R0 ? rx[i + 1] - 1 : L - 1;
+        const int len = stop - rx[i] + 1;
+        ry[i] = stop;
+        rw[i] = rz[i] ? len : len * wf;  // Region::set_weight :48-54
+        nx[i] = i + 1 < R0 ? i + 1 : -1;
+        pv[i] = i - 1;
+    }
+    __syncthreads();
+    int R = R0;
+    while (R >= 2) {
+        int bw = 0x7fffffff, bi = 0x7fffffff;
+        for (int i = lane; i < R0; i += 64) {
+            const int wt = rw[i];
+            if (wt >= 0 && wt < bw) {
+                bw = wt;
+                bi = i;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int ow = __shfl_xor(bw, o), oi = __shfl_xor(bi, o);
+            if (ow < bw || (ow == bw && oi < bi)) {
+                bw = ow;
+                bi = oi;
+            }
+        }
+        if (bw >= min_length) break;
+        const int mi = bi, p = pv[mi], q = nx[mi];
+        const int keep = p >= 0 ? p : mi;
+        const int nw = rw[mi] + (p >= 0 ? rw[p] : 0) + (q >= 0 ? rw[q] : 0);
+        const int x = p >= 0 ? rx[p] : rx[mi], y = q >= 0 ? ry[q] : ry[mi], z = rz[mi] == 0 ? 1 : 0;
+        const int after = q >= 0 ? nx[q] : nx[mi];
+        __syncthreads();
+        if (lane == 0) {
+            if (p >= 0) rw[mi] = -1;
+            if (q >= 0) rw[q] = -1;
+            rx[keep] = x;
+            ry[keep] = y;
+            rz[keep] = z;
+            rw[keep] = nw;
+            nx[keep] = after;
+            if (after >= 0) pv[after] = keep;
+        }
+        __syncthreads();
+        R -= (p >= 0) + (q >= 0);
+    }
+    // survivors, in order
+    k = 0;
+    for (int base = 0; base < R0; base += 64) {
+        const int i = base + lane;
+        const bool a = i < R0 && rw[i] >= 0;
+        const unsigned long long m = ballot(a);
+        if (a) out[k + __popcll(m & ((1ull << lane) - 1ull))] = make_int4(rx[i], ry[i], rz[i], rw[i]);
+        k += __popcll(m);
+    }
+    __syncthreads();
+    return R;
+}
+
 // AbstractAligner.cpp:89-102: drop columns that are '-' in every row
 __device__ int remove_pure_gap_cols(const WaveCtx& w, char* buf, int cap, int L) {
     int dest = 0;
@@ -354,6 +449,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
         const long long t_job = clock64();
         long long t_ph[3] = {0, 0, 0}, st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        long long t_regions = 0;
+        int st_regions0 = 0;
         int st_calls = 0, st_shifts = 0, st_gaps = 0, st_regions = 0, st_fast = 0;
         WaveCtx w;
         w.lane = lane;
@@ -427,14 +524,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 // 2. fix_bad_regions
                 int4 rreg = make_int4(0, 0, 0, 0);
                 unsigned long long gmask = 0;
+                const long long t_reg0 = clock64();
                 int R = regions_in_registers(w, A, cap, L0, a.P.wf, a.P.min_length, rreg, gmask, (int*)S.good_col);
                 const bool fast = R >= 0;
                 if (!fast) {
                     count_equal_cols(w, A, cap, 0, L0, S.good_col);
                     __syncthreads();
-                    R = make_regions(w, S.good_col, L0, a.P.wf, S.regions);
-                    R = reduce_regions(w, S.regions, R, a.P.min_length);
+                    R = regions_in_lds(w, S.good_col, L0, a.P.wf, a.P.min_length, (LdsInt*)stage, a.stage_bytes,
+                                       S.regions);
+                    if (R < 0) {
+                        R = make_regions(w, S.good_col, L0, a.P.wf, S.regions);
+                        st_regions0 = R;
+                        R = reduce_regions(w, S.regions, R, a.P.min_length);
+                    }
                 }
+                t_regions = clock64() - t_reg0;
                 st_regions = R;
                 int colB = 0;
                 if (fast && R == 1 && __shfl(rreg.z, 0)) {  // one good region: the alignment stays in A
@@ -536,7 +640,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             js[10] = t_ph[2];
             js[11] = clock64() - t_rg;
             for (int q = 0; q < 10; q++) js[12 + q] = st_prof[q];
-            for (int q = 22; q < NPGX_JOB_STATS; q++) js[q] = 0;
+            js[22] = t_regions;
+            js[23] = st_regions0;
         }
         __syncthreads();
     }

@@ -78,12 +78,33 @@ struct SaArgs {
 __device__ int count_equal_cols(const WaveCtx& w, const char* buf, int cap, int c0, int c1,
                                 unsigned char* flags) {
     int cnt = 0;
-    for (int c = c0 + w.lane; c < c1; c += 64) {
-        const char x = buf[c];
-        bool eq = true;
-        for (int r = 1; r < w.n; r++) eq &= (buf[(size_t)r * cap + c] == x);
-        cnt += eq;
-        if (flags) flags[c] = eq;
+    for (int b = c0; b < c1; b += 256) {  // four 64-column chunks per step: four loads in flight
+        char x[4];
+        bool eq[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = b + u * 64 + w.lane;
+            eq[u] = c < c1;
+            x[u] = eq[u] ? buf[c] : 0;
+        }
+        for (int r = 1; r < w.n; r++) {
+            char y[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int c = b + u * 64 + w.lane;
+                y[u] = c < c1 ? buf[(size_t)r * cap + c] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) eq[u] &= y[u] == x[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = b + u * 64 + w.lane;
+            if (c < c1) {
+                cnt += eq[u];
+                if (flags) flags[c] = eq[u];
+            }
+        }
     }
     return wave_sum(cnt);
 }
@@ -282,37 +303,80 @@ __device__ int regions_in_registers(const WaveCtx& w, const char* A, int cap, in
 
 typedef __attribute__((address_space(3))) int LdsInt;
 
-// make_regions (:62-80) + reduce_regions (:121-130) for long alignments, in
-// LDS (the job's row stage, free after process_seqs): regions as arrays with
-// prev/next links; a merge rewrites the surviving region and unlinks the
-// others (no shifting); the minimum is a wave-parallel scan over the array
-// (alive entries keep their order, so the lowest index is the reference's
-// first minimum).  The survivors go to `out` in order; returns their count,
-// or -1 when the LDS area is too small.
-__device__ int regions_in_lds(const WaveCtx& w, const unsigned char* good, int L, int wf, int min_length,
-                              LdsInt* area, int area_bytes, int4* out) {
+// count_equal_cols flags (:416-426) + make_regions (:62-80) + reduce_regions
+// (:121-130) for long alignments, in LDS (the job's row stage, free after
+// process_seqs): identical-column flags as one bit per column, regions as
+// arrays with prev/next links; a merge rewrites the surviving region and
+// unlinks the others (no shifting); the minimum is a wave-parallel scan (alive
+// entries keep their order, so the lowest index is the reference's first
+// minimum).  The survivors go to `out` in order with .w = the number of
+// identical columns in the region (score_of before re-alignment); returns
+// their count, or -1 when the LDS area is too small.
+__device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, int wf, int min_length,
+                              char* area_g, int area_bytes, int4* out) {
+    typedef __attribute__((address_space(3))) unsigned long long LdsU64w;
     const int lane = w.lane;
-    // count region starts first
-    int R0 = 0;
-    for (int base = 0; base < L; base += 64) {
-        const int j = base + lane;
-        const bool b = j < L && (j == 0 || good[j] != good[j - 1]);
-        R0 += __popcll(ballot(b));
-    }
-    if ((long long)R0 * 24 > area_bytes) return -1;
-    LdsInt *rx = area, *ry = area + R0, *rz = area + 2 * R0, *rw = area + 3 * R0, *nx = area + 4 * R0,
-           *pv = area + 5 * R0;
-    int k = 0;
-    for (int base = 0; base < L; base += 64) {
-        const int j = base + lane;
-        const bool b = j < L && (j == 0 || good[j] != good[j - 1]);
-        const unsigned long long m = ballot(b);
-        if (b) {
-            const int i = k + __popcll(m & ((1ull << lane) - 1ull));
-            rx[i] = j;
-            rz[i] = good[j];
+    const int nw = (L + 63) >> 6;
+    if ((long long)nw * 16 > area_bytes) return -1;
+    LdsU64w* gm = (LdsU64w*)area_g;  // identical-column bits
+    LdsU64w* sm = gm + nw;           // region-start bits
+    for (int b = 0; b < nw; b += 4) {
+        bool eq[4];
+        char x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = (b + u) * 64 + lane;
+            eq[u] = c < L;
+            x[u] = eq[u] ? A[c] : 0;
         }
-        k += __popcll(m);
+        for (int r = 1; r < w.n; r++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int c = (b + u) * 64 + lane;
+                eq[u] &= (c < L ? A[(size_t)r * cap + c] : 0) == x[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned long long m = ballot(eq[u]);
+            if (lane == 0 && b + u < nw) gm[b + u] = m;
+        }
+    }
+    __syncthreads();
+    int R0 = 0;
+    for (int q = lane; q < nw; q += 64) {
+        const unsigned long long g = gm[q];
+        const unsigned long long valid = (q < nw - 1 || (L & 63) == 0) ? ~0ull : ((1ull << (L & 63)) - 1);
+        unsigned long long st = (g ^ ((g << 1) | (q > 0 ? (gm[q - 1] >> 63) : (g & 1ull)))) & valid;
+        if (q == 0) st |= 1ull;
+        sm[q] = st;
+        R0 += __popcll(st);
+    }
+    R0 = wave_sum(R0);
+    __syncthreads();
+    const long long need = (long long)nw * 16 + (long long)R0 * 24;
+    if (need > area_bytes) return -1;
+    LdsInt* rx = (LdsInt*)(sm + nw);
+    LdsInt *ry = rx + R0, *rz = rx + 2 * R0, *rw = rx + 3 * R0, *nx = rx + 4 * R0, *pv = rx + 5 * R0;
+    int k = 0;
+    for (int q0 = 0; q0 < nw; q0 += 64) {  // region starts in order: word prefix counts
+        const int q = q0 + lane;
+        unsigned long long st = q < nw ? sm[q] : 0ull;
+        const int c = __popcll(st);
+        int pre = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(pre, o);
+            if (lane >= o) pre += t;
+        }
+        int i = k + pre - c;
+        for (; st; st &= st - 1) {
+            const int j = q * 64 + __ffsll((long long)st) - 1;
+            rx[i] = j;
+            rz[i] = (int)((gm[q] >> (j & 63)) & 1ull);
+            i++;
+        }
+        k += __shfl(pre, 63);
     }
     __syncthreads();
     for (int i = lane; i < R0; i += 64) {
@@ -345,7 +409,7 @@ __device__ int regions_in_lds(const WaveCtx& w, const unsigned char* good, int L
         if (bw >= min_length) break;
         const int mi = bi, p = pv[mi], q = nx[mi];
         const int keep = p >= 0 ? p : mi;
-        const int nw = rw[mi] + (p >= 0 ? rw[p] : 0) + (q >= 0 ? rw[q] : 0);
+        const int nwt = rw[mi] + (p >= 0 ? rw[p] : 0) + (q >= 0 ? rw[q] : 0);
         const int x = p >= 0 ? rx[p] : rx[mi], y = q >= 0 ? ry[q] : ry[mi], z = rz[mi] == 0 ? 1 : 0;
         const int after = q >= 0 ? nx[q] : nx[mi];
         __syncthreads();
@@ -355,20 +419,30 @@ __device__ int regions_in_lds(const WaveCtx& w, const unsigned char* good, int L
             rx[keep] = x;
             ry[keep] = y;
             rz[keep] = z;
-            rw[keep] = nw;
+            rw[keep] = nwt;
             nx[keep] = after;
             if (after >= 0) pv[after] = keep;
         }
         __syncthreads();
         R -= (p >= 0) + (q >= 0);
     }
-    // survivors, in order
+    // survivors in order, with their identical-column counts
     k = 0;
     for (int base = 0; base < R0; base += 64) {
         const int i = base + lane;
-        const bool a = i < R0 && rw[i] >= 0;
-        const unsigned long long m = ballot(a);
-        if (a) out[k + __popcll(m & ((1ull << lane) - 1ull))] = make_int4(rx[i], ry[i], rz[i], rw[i]);
+        const bool alive = i < R0 && rw[i] >= 0;
+        int4 rg = make_int4(0, 0, 0, 0);
+        if (alive) {
+            rg = make_int4(rx[i], ry[i], rz[i], 0);
+            int cnt = 0;
+            for (int q = rg.x >> 6; q <= (rg.y >> 6); q++) {
+                const int lo = q == (rg.x >> 6) ? (rg.x & 63) : 0, hi = q == (rg.y >> 6) ? (rg.y & 63) : 63;
+                cnt += __popcll(gm[q] & ((hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo)));
+            }
+            rg.w = cnt;
+        }
+        const unsigned long long m = ballot(alive);
+        if (alive) out[k + __popcll(m & ((1ull << lane) - 1ull))] = rg;
         k += __popcll(m);
     }
     __syncthreads();
@@ -378,27 +452,48 @@ __device__ int regions_in_lds(const WaveCtx& w, const unsigned char* good, int L
 // AbstractAligner.cpp:89-102: drop columns that are '-' in every row
 __device__ int remove_pure_gap_cols(const WaveCtx& w, char* buf, int cap, int L) {
     int dest = 0;
-    for (int base = 0; base < L; base += 64) {
-        const int c = base + w.lane;
-        bool keep = false;
-        if (c < L)
-            for (int r = 0; r < w.n && !keep; r++) keep = buf[(size_t)r * cap + c] != '-';
-        const unsigned long long km = ballot(keep);
-        if (km == ((base + 64 <= L) ? ~0ull : ((1ull << (L - base)) - 1ull)) && dest == base) {
-            dest += __popcll(km);  // nothing removed so far
-            continue;
+    for (int b = 0; b < L; b += 256) {
+        // keep flags of four chunks: row 0 first (four loads in flight), the
+        // other rows only where row 0 has a gap
+        bool keep[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = b + u * 64 + w.lane;
+            keep[u] = c < L && buf[c] != '-';
         }
-        __syncthreads();
-        // move kept columns of this chunk left (row by row, lanes = columns)
-        const int to = dest + __popcll(km & ((1ull << w.lane) - 1ull));
-        for (int r = 0; r < w.n; r++) {
-            char x = 0;
-            if (keep) x = buf[(size_t)r * cap + c];
-            __syncthreads();
-            if (keep) buf[(size_t)r * cap + to] = x;
-            __syncthreads();
+        for (int r = 1; r < w.n; r++) {
+            bool need = false;
+#pragma unroll
+            for (int u = 0; u < 4; u++) need |= (b + u * 64 + w.lane < L) && !keep[u];
+            if (!any_lane(WaveCtx{w.lane, w.n, ~0ull, true}, need)) break;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int c = b + u * 64 + w.lane;
+                if (c < L && !keep[u]) keep[u] = buf[(size_t)r * cap + c] != '-';
+            }
         }
-        dest += __popcll(km);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int base = b + u * 64;
+            if (base >= L) break;
+            const int c = base + w.lane;
+            const unsigned long long km = ballot(keep[u]);
+            if (km == ((base + 64 <= L) ? ~0ull : ((1ull << (L - base)) - 1ull)) && dest == base) {
+                dest += __popcll(km);  // nothing removed so far
+                continue;
+            }
+            __syncthreads();
+            // move kept columns of this chunk left (row by row, lanes = columns)
+            const int to = dest + __popcll(km & ((1ull << w.lane) - 1ull));
+            for (int r = 0; r < w.n; r++) {
+                char x = 0;
+                if (keep[u]) x = buf[(size_t)r * cap + c];
+                __syncthreads();
+                if (keep[u]) buf[(size_t)r * cap + to] = x;
+                __syncthreads();
+            }
+            dest += __popcll(km);
+        }
     }
     return dest;
 }
@@ -527,12 +622,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 const long long t_reg0 = clock64();
                 int R = regions_in_registers(w, A, cap, L0, a.P.wf, a.P.min_length, rreg, gmask, (int*)S.good_col);
                 const bool fast = R >= 0;
+                bool counted = false;  // S.regions[].w holds each region's identical columns
                 if (!fast) {
-                    count_equal_cols(w, A, cap, 0, L0, S.good_col);
-                    __syncthreads();
-                    R = regions_in_lds(w, S.good_col, L0, a.P.wf, a.P.min_length, (LdsInt*)stage, a.stage_bytes,
-                                       S.regions);
+                    R = regions_in_lds(w, A, cap, L0, a.P.wf, a.P.min_length, stage, a.stage_bytes, S.regions);
+                    counted = R >= 0;
                     if (R < 0) {
+                        count_equal_cols(w, A, cap, 0, L0, S.good_col);
+                        __syncthreads();
                         R = make_regions(w, S.good_col, L0, a.P.wf, S.regions);
                         st_regions0 = R;
                         R = reduce_regions(w, S.regions, R, a.P.min_length);
@@ -570,10 +666,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                 (a1 == 63 ? ~0ull : ((1ull << (a1 + 1)) - 1)) & (~0ull << a0);
                             before = __popcll(gmask & m);
                         }
+                        before = wave_sum(before);
+                    } else if (counted) {
+                        before = rg.w;
                     } else {
                         for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
+                        before = wave_sum(before);
                     }
-                    before = wave_sum(before);
                     const View cv = stage_segment(w, A, cap, C, stage, a.stage_bytes, rg.x, rg.y + 1);
                     const int Lc = pr.run(cv, colB);
                     if (any_lane(w, pr.ovf)) {

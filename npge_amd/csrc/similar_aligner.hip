@@ -354,10 +354,13 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
     }
     R0 = wave_sum(R0);
     __syncthreads();
-    const long long need = (long long)nw * 16 + (long long)R0 * 24;
-    if (need > area_bytes) return -1;
+    // per region 12 bytes: start (-1: merged away), weight | good << 31, and
+    // next | prev << 16 (0xFFFF: none); a region ends where the next alive starts
+    const long long need = (long long)nw * 16 + (long long)R0 * 12;
+    if (need > area_bytes || R0 >= 0xFFFF) return -1;
     LdsInt* rx = (LdsInt*)(sm + nw);
-    LdsInt *ry = rx + R0, *rz = rx + 2 * R0, *rw = rx + 3 * R0, *nx = rx + 4 * R0, *pv = rx + 5 * R0;
+    LdsInt* rw = rx + R0;
+    LdsInt* lk = rx + 2 * R0;
     int k = 0;
     for (int q0 = 0; q0 < nw; q0 += 64) {  // region starts in order: word prefix counts
         const int q = q0 + lane;
@@ -373,27 +376,26 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
         for (; st; st &= st - 1) {
             const int j = q * 64 + __ffsll((long long)st) - 1;
             rx[i] = j;
-            rz[i] = (int)((gm[q] >> (j & 63)) & 1ull);
+            rw[i] = (int)((gm[q] >> (j & 63)) & 1ull) << 31;  // good flag; weight below
             i++;
         }
         k += __shfl(pre, 63);
     }
     __syncthreads();
     for (int i = lane; i < R0; i += 64) {
-        const int stop = i + 1 < R0 ? rx[i + 1] - 1 : L - 1;
-        const int len = stop - rx[i] + 1;
-        ry[i] = stop;
-        rw[i] = rz[i] ? len : len * wf;  // Region::set_weight :48-54
-        nx[i] = i + 1 < R0 ? i + 1 : -1;
-        pv[i] = i - 1;
+        const int len = (i + 1 < R0 ? rx[i + 1] : L) - rx[i];
+        const int good = (int)((unsigned)rw[i] >> 31);
+        rw[i] = (good << 31) | (good ? len : len * wf);  // Region::set_weight :48-54
+        lk[i] = (i + 1 < R0 ? i + 1 : 0xFFFF) | ((i > 0 ? i - 1 : 0xFFFF) << 16);
     }
     __syncthreads();
+    const int WM = 0x7fffffff;
     int R = R0;
     while (R >= 2) {
-        int bw = 0x7fffffff, bi = 0x7fffffff;
+        int bw = WM, bi = WM;
         for (int i = lane; i < R0; i += 64) {
-            const int wt = rw[i];
-            if (wt >= 0 && wt < bw) {
+            const int wt = rw[i] & WM;
+            if (rx[i] >= 0 && wt < bw) {
                 bw = wt;
                 bi = i;
             }
@@ -407,33 +409,34 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
             }
         }
         if (bw >= min_length) break;
-        const int mi = bi, p = pv[mi], q = nx[mi];
-        const int keep = p >= 0 ? p : mi;
-        const int nwt = rw[mi] + (p >= 0 ? rw[p] : 0) + (q >= 0 ? rw[q] : 0);
-        const int x = p >= 0 ? rx[p] : rx[mi], y = q >= 0 ? ry[q] : ry[mi], z = rz[mi] == 0 ? 1 : 0;
-        const int after = q >= 0 ? nx[q] : nx[mi];
+        const int mi = bi, l = lk[mi];
+        const int p = (l >> 16) & 0xFFFF, q = l & 0xFFFF;
+        const bool hp = p != 0xFFFF, hq = q != 0xFFFF;
+        const int keep = hp ? p : mi;
+        const int nwt = (rw[mi] & WM) + (hp ? rw[p] & WM : 0) + (hq ? rw[q] & WM : 0);
+        const int z = ((unsigned)rw[mi] >> 31) ? 0 : 1;
+        const int after = hq ? lk[q] & 0xFFFF : q;
+        const int keep_prev = (lk[keep] >> 16) & 0xFFFF;
         __syncthreads();
         if (lane == 0) {
-            if (p >= 0) rw[mi] = -1;
-            if (q >= 0) rw[q] = -1;
-            rx[keep] = x;
-            ry[keep] = y;
-            rz[keep] = z;
-            rw[keep] = nwt;
-            nx[keep] = after;
-            if (after >= 0) pv[after] = keep;
+            if (hp) rx[mi] = -1;
+            if (hq) rx[q] = -1;
+            rw[keep] = (z << 31) | nwt;
+            lk[keep] = after | (keep_prev << 16);
+            if (after != 0xFFFF) lk[after] = (lk[after] & 0xFFFF) | (keep << 16);
         }
         __syncthreads();
-        R -= (p >= 0) + (q >= 0);
+        R -= (int)hp + (int)hq;
     }
     // survivors in order, with their identical-column counts
     k = 0;
     for (int base = 0; base < R0; base += 64) {
         const int i = base + lane;
-        const bool alive = i < R0 && rw[i] >= 0;
+        const bool alive = i < R0 && rx[i] >= 0;
         int4 rg = make_int4(0, 0, 0, 0);
         if (alive) {
-            rg = make_int4(rx[i], ry[i], rz[i], 0);
+            const int nxt = lk[i] & 0xFFFF;
+            rg = make_int4(rx[i], (nxt != 0xFFFF ? rx[nxt] : L) - 1, (int)((unsigned)rw[i] >> 31), 0);
             int cnt = 0;
             for (int q = rg.x >> 6; q <= (rg.y >> 6); q++) {
                 const int lo = q == (rg.x >> 6) ? (rg.x & 63) : 0, hi = q == (rg.y >> 6) ? (rg.y & 63) : 63;

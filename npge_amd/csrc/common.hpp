@@ -82,6 +82,8 @@ struct DevBuf {
         }
         return p;
     }
+    // ensure() with 1.5x headroom for buffers whose size varies from call to call
+    T* grow(size_t n) { return ensure(n > cap ? std::max(n, cap + cap / 2) : n); }
 };
 
 // Pinned host staging for async copies (bump allocated; when full, the stream

@@ -38,6 +38,18 @@ struct SaJob {
     int64_t scratch;    // byte offset of this job's A|B|C scratch
     int32_t n;          // non-empty rows (<= 64)
     int32_t cap;        // column capacity of A, B and C rows
+    int64_t reg_off;    // first entry of the job's region list (deferred fix_bad_regions)
+    int32_t reg_cap;    // entries available there
+    int32_t pad;
+};
+
+// One bad region of a deferred job, re-aligned as a job of its own
+// (fix_bad_regions :428-459): rows = the region's gap-filtered reversed
+// segments, written by the parent into its C at column x.
+struct SaSub {
+    int32_t job, x;
+    int32_t out_cap, pad;
+    int64_t out_off;    // byte offset in the sub-job output pool (n rows x out_cap)
 };
 
 struct SaArgs {
@@ -72,6 +84,18 @@ struct SaArgs {
     int32_t words_bytes;       // LDS bytes of the chunk words / code history
     uint32_t ltab_log2;        // LDS word-table entries (log2)
     Params P;
+    // deferred fix_bad_regions (attempt 0): regions and sub-jobs
+    int32_t defer;             // > 0: defer the bad regions of alignments of at least this many columns
+    int4* job_regions;         // per job: x, y, good (1) or -(sub+1), identical columns before
+    int32_t* job_nreg;         // regions per deferred job
+    SaSub* subs;
+    int2* sub_res;             // per sub-job: columns (-1: overflow), identical columns after
+    unsigned long long* alloc; // [0] pool bytes taken, [1] sub-jobs issued
+    unsigned int* counters;    // [0] next sub-job, [1] deferred jobs, [2] next deferred job
+    unsigned char* pool;       // per sub-job: 64 row lengths (int32), then n rows x out_cap
+    int64_t pool_cap;
+    int64_t max_sub;
+    int32_t* fin;              // the deferred jobs
 };
 
 // number of columns c in [c0, c1) identical over all rows (score_of :416-426)
@@ -391,25 +415,9 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
     __syncthreads();
     const int WM = 0x7fffffff;
     int R = R0;
-    while (R >= 2) {
-        int bw = WM, bi = WM;
-        for (int i = lane; i < R0; i += 64) {
-            const int wt = rw[i] & WM;
-            if (rx[i] >= 0 && wt < bw) {
-                bw = wt;
-                bi = i;
-            }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const int ow = __shfl_xor(bw, o), oi = __shfl_xor(bi, o);
-            if (ow < bw || (ow == bw && oi < bi)) {
-                bw = ow;
-                bi = oi;
-            }
-        }
-        if (bw >= min_length) break;
-        const int mi = bi, l = lk[mi];
+    // one merge of the minimum region mi with its alive neighbours (merge_region :94-119)
+    auto merge = [&](int mi, int& hp_out, int& hq_out, int& p_out, int& q_out) {
+        const int l = lk[mi];
         const int p = (l >> 16) & 0xFFFF, q = l & 0xFFFF;
         const bool hp = p != 0xFFFF, hq = q != 0xFFFF;
         const int keep = hp ? p : mi;
@@ -426,7 +434,78 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
             if (after != 0xFFFF) lk[after] = (lk[after] & 0xFFFF) | (keep << 16);
         }
         __syncthreads();
-        R -= (int)hp + (int)hq;
+        hp_out = hp;
+        hq_out = hq;
+        p_out = p;
+        q_out = q;
+    };
+    const int nb = (R0 + 63) >> 6;
+    if (nb <= 256) {
+        // minimum of every 64-entry block in registers (lane l: blocks l + 64k):
+        // a step reads the block minima, merges, and rescans only the blocks
+        // whose entries changed
+        int bm[4], bi[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            bm[k] = WM;
+            bi[k] = WM;
+        }
+        auto rescan = [&](int b) {
+            const int i = b * 64 + lane;
+            const bool alive = i < R0 && rx[i] >= 0;
+            const int wt = alive ? rw[i] & WM : WM;
+            const int mw = wave_min(wt);
+            const unsigned long long m = ballot(alive && wt == mw);
+            const int first = m ? b * 64 + __ffsll((long long)m) - 1 : WM;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (lane == (b & 63) && k == (b >> 6)) {
+                    bm[k] = m ? mw : WM;
+                    bi[k] = first;
+                }
+        };
+        for (int b = 0; b < nb; b++) rescan(b);
+        while (R >= 2) {
+            const int bw = wave_min(min(min(bm[0], bm[1]), min(bm[2], bm[3])));
+            if (bw >= min_length) break;
+            // first minimum: lowest block, i.e. lowest k, then lowest lane
+            int mi = WM;
+#pragma unroll
+            for (int k = 3; k >= 0; k--) {
+                const unsigned long long m = ballot(bm[k] == bw);
+                if (m) mi = __shfl(bi[k], __ffsll((long long)m) - 1);
+            }
+            int hp, hq, p, q;
+            merge(mi, hp, hq, p, q);
+            R -= hp + hq;
+            const int b0 = mi >> 6, b1 = hp ? p >> 6 : b0, b2 = hq ? q >> 6 : b0;
+            rescan(b0);
+            if (b1 != b0) rescan(b1);
+            if (b2 != b0 && b2 != b1) rescan(b2);
+        }
+    } else {
+        while (R >= 2) {
+            int bw = WM, bi = WM;
+            for (int i = lane; i < R0; i += 64) {
+                const int wt = rw[i] & WM;
+                if (rx[i] >= 0 && wt < bw) {
+                    bw = wt;
+                    bi = i;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const int ow = __shfl_xor(bw, o), oi = __shfl_xor(bi, o);
+                if (ow < bw || (ow == bw && oi < bi)) {
+                    bw = ow;
+                    bi = oi;
+                }
+            }
+            if (bw >= min_length) break;
+            int hp, hq, p, q;
+            merge(bi, hp, hq, p, q);
+            R -= hp + hq;
+        }
     }
     // survivors in order, with their identical-column counts
     k = 0;
@@ -499,6 +578,327 @@ __device__ int remove_pure_gap_cols(const WaveCtx& w, char* buf, int cap, int L)
         }
     }
     return dest;
+}
+
+// take n units of a bounded counter; -1 when they do not fit (the counter
+// still advances: later requests fail too, nothing is handed out twice)
+__device__ __forceinline__ long long reserve(unsigned long long* ctr, unsigned long long n, unsigned long long cap) {
+    const unsigned long long old = atomicAdd(ctr, n);
+    return old + n > cap ? -1 : (long long)old;
+}
+
+__device__ __forceinline__ int sub_out_cap(int cap, int width) { return min(cap, (2 * width + 64 + 15) & ~15); }
+
+__device__ __forceinline__ int64_t sub_bytes(int n, int out_cap) {
+    return (256 + (int64_t)n * out_cap + 255) & ~255ll;
+}
+
+// fix_bad_regions (:428-459), deferred: the regions go to the job's list with
+// each bad region's identical columns, every bad region's gap-filtered
+// reversed rows to C at its own columns, and the bad regions become sub-jobs
+// realigned GPU-wide by k_align_sub; k_align_finish assembles the job.
+// Returns false (nothing deferred: realign inline) when the lists or the
+// sub-job pool are full.
+// (DeferOut instead of SaArgs: no copy of the kernel arguments to the stack)
+struct DeferOut {  // the SaArgs fields defer_regions writes
+    int4* job_regions;
+    int32_t* job_nreg;
+    SaSub* subs;
+    unsigned long long* alloc;
+    unsigned int* counters;
+    unsigned char* pool;
+    int64_t pool_cap, max_sub;
+    int32_t* fin;
+};
+
+__device__ __forceinline__ bool defer_regions(const DeferOut a, int n, int j, int64_t reg_off, int reg_cap,
+                                           const char* A, char* C, int cap, int R, bool fast, bool counted,
+                                           int4 rreg, unsigned long long gmask, const int4* regions,
+                                           const unsigned char* good_col) {
+    WaveCtx w;
+    const int lane = threadIdx.x;
+    w.lane = lane;
+    w.n = n;
+    w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    w.act = lane < n;
+    if (R > reg_cap) return false;
+    int4* jr = a.job_regions + reg_off;
+    int nbad = 0;
+    int64_t need = 0;
+    for (int ri = 0; ri < R; ri++) {
+        const int4 rg = fast ? make_int4(__shfl(rreg.x, ri), __shfl(rreg.y, ri), __shfl(rreg.z, ri),
+                                         __shfl(rreg.w, ri))
+                             : regions[ri];
+        int before = 0;
+        if (!rg.z) {
+            if (fast) {
+                const int lo = lane * 64, hi = lo + 63;
+                if (lo <= rg.y && hi >= rg.x) {
+                    const int a0 = max(rg.x, lo) - lo, a1 = min(rg.y, hi) - lo;
+                    before = __popcll(gmask & ((a1 == 63 ? ~0ull : ((1ull << (a1 + 1)) - 1)) & (~0ull << a0)));
+                }
+                before = wave_sum(before);
+            } else if (counted) {
+                before = rg.w;
+            } else {
+                for (int c = rg.x + lane; c <= rg.y; c += 64) before += good_col[c];
+                before = wave_sum(before);
+            }
+            nbad++;
+            need += sub_bytes(w.n, sub_out_cap(cap, rg.y - rg.x + 1));
+        }
+        if (lane == 0) jr[ri] = make_int4(rg.x, rg.y, rg.z ? 1 : 0, before);
+    }
+    if (nbad == 0) return false;
+    long long base = 0, s0 = 0;
+    if (lane == 0) {
+        base = reserve(&a.alloc[0], (unsigned long long)need, (unsigned long long)a.pool_cap);
+        if (base >= 0) s0 = (long long)atomicAdd(&a.alloc[1], (unsigned long long)nbad);  // max_sub bounds every job's bad regions
+    }
+    base = (long long)shfl64((unsigned long long)base, 0);
+    s0 = (long long)shfl64((unsigned long long)s0, 0);
+    __syncthreads();
+    if (base < 0) return false;
+    int64_t off = base;
+    int k = 0;
+    for (int ri = 0; ri < R; ri++) {
+        const int4 rg = jr[ri];
+        if (rg.z) continue;
+        const int out_cap = sub_out_cap(cap, rg.y - rg.x + 1);
+        const View cv = filter_reverse(w, A, cap, C + rg.x, cap, rg.x, rg.y + 1);
+        const long long sub = s0 + k++;
+        if (w.act) ((int*)(a.pool + off))[lane] = cv.len;
+        if (lane == 0) {
+            SaSub d;
+            d.job = j;
+            d.x = rg.x;
+            d.out_cap = out_cap;
+            d.pad = 0;
+            d.out_off = off;
+            a.subs[sub] = d;
+            jr[ri] = make_int4(rg.x, rg.y, -(int)(sub + 1), rg.w);
+        }
+        off += sub_bytes(w.n, out_cap);
+    }
+    if (lane == 0) {
+        a.job_nreg[j] = R;
+        a.fin[atomicAdd(&a.counters[1], 1u)] = j;
+    }
+    __syncthreads();
+    return true;
+}
+
+// first word-table epoch of a follow-up kernel: above every epoch the
+// previous launches used
+__device__ __forceinline__ uint32_t next_epoch(const SaArgs& a) {
+    return max(a.epoch_base, atomicMax(a.slot_epoch, 0u) + 1u);
+}
+
+// slot setup shared by the three aligner kernels (same LDS layout)
+struct SlotEnv {
+    Slot S;
+    char* stage;
+};
+
+__device__ __forceinline__ SlotEnv slot_env(const SaArgs& a, unsigned long long* lds_u64) {
+    SlotEnv e;
+    Slot& S = e.S;
+    const int lane = threadIdx.x;
+    const uint32_t ltab = 1u << a.ltab_log2;
+    S.lkeys = lds_u64;
+    S.lmask = lds_u64 + ltab;
+    S.ltab_log2 = a.ltab_log2;
+    S.lwords = lds_u64 + 2 * ltab;
+    S.hist_cap = a.hist_cap;
+    for (uint32_t i = lane; i < ltab; i += 64) lds_u64[i] = 0ull;
+    __syncthreads();
+    e.stage = (char*)(lds_u64 + 2 * ltab) + a.words_bytes;
+    const size_t slot = blockIdx.x;
+    const size_t tcap = (size_t)1 << a.tcap_log2;
+    S.tkeys = a.tkeys + slot * tcap;
+    S.tmask = a.tmask + slot * tcap;
+    S.tcap_log2 = a.tcap_log2;
+    const size_t stn = (size_t)a.st_depth_max * 64;
+    S.st_p = a.st_p + slot * stn;
+    S.st_len = a.st_len + slot * stn;
+    S.st_pos = a.st_pos + slot * stn;
+    S.st_col = a.st_col + slot * a.st_depth_max;
+    S.st_depth_max = a.st_depth_max;
+    S.regions = a.regions + slot * (size_t)a.slot_cols;
+    S.good_col = a.good_col + slot * (size_t)a.slot_cols;
+    return e;
+}
+
+// rows of a view set into LDS when they fit (every char(q) then an LDS read)
+__device__ __forceinline__ void stage_rows(View& v0, int n, char* stage, int stage_bytes) {
+    const int lane = threadIdx.x;
+    int off = 0, tot = 0;
+    for (int r = 0; r < n; r++) {
+        const int lr = __shfl(v0.len, r);
+        if (lane == r) off = tot;
+        tot += lr;
+    }
+    if (tot > stage_bytes) return;
+    for (int r = 0; r < n; r++) {
+        const char* src = shfl_ptr(v0.p, r);
+        const int lr = __shfl(v0.len, r), o = __shfl(off, r);
+        for (int base = 0; base < lr; base += 64 * 8) {
+            char x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int q = base + u * 64 + lane;
+                x[u] = q < lr ? src[q] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int q = base + u * 64 + lane;
+                if (q < lr) stage[o + q] = x[u];
+            }
+        }
+    }
+    __syncthreads();
+    if (lane < n) v0.p = stage + off;
+}
+
+// realing_end (:461-484) on B + AbstractAligner remove_gaps; returns the length
+__device__ int finish_tail(Proc& pr, const WaveCtx& w, char* B, char* C, int cap, int L, char* stage,
+                           int stage_bytes, int ac, bool& ovf) {
+    pr.ob = B;
+    if (!ovf && L >= 2) {
+        int prefix = L - ac;
+        if (prefix < 1) prefix = 1;
+        const View tv = stage_segment(w, B, cap, C, stage, stage_bytes, prefix, L);
+        const int Lt = pr.run(tv, prefix);
+        if (any_lane(w, pr.ovf)) ovf = true;
+        else {
+            cm_reverse(w, B, cap, prefix, prefix + Lt);
+            L = prefix + Lt;
+        }
+    }
+    __syncthreads();
+    if (!ovf) L = remove_pure_gap_cols(w, B, cap, L);
+    return L;
+}
+
+// k_align_sub: every bad region of every deferred job, one wave each
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_sub(SaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
+    const int lane = threadIdx.x;
+    SlotEnv e = slot_env(a, lds_u64);
+    uint32_t epoch = next_epoch(a), lepoch = 0;
+    const unsigned int n_sub = (unsigned int)a.alloc[1];
+    while (true) {
+        unsigned int sn = 0;
+        if (lane == 0) sn = atomicAdd(&a.counters[0], 1u);
+        sn = __shfl(sn, 0);
+        if (sn >= n_sub) break;
+        const SaSub d = a.subs[sn];
+        const SaJob job = a.jobs[d.job];
+        const int n = job.n, cap = job.cap;
+        WaveCtx w;
+        w.lane = lane;
+        w.n = n;
+        w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+        w.act = lane < n;
+        char* C = (char*)(a.scratch + job.scratch) + 2ll * n * cap;
+        View v{nullptr, 0, 1};
+        if (w.act) {
+            v.p = C + (size_t)lane * cap + d.x;
+            v.len = ((const int*)(a.pool + d.out_off))[lane];
+        }
+        stage_rows(v, n, e.stage, a.stage_bytes);
+        char* out = (char*)(a.pool + d.out_off + 256);
+        Proc pr(w, a.P, e.S, out, d.out_cap, epoch, lepoch);
+        const int Lc = pr.run(v, 0);
+        const bool ovf = any_lane(w, pr.ovf);
+        __syncthreads();
+        const int after = ovf ? 0 : count_equal_cols(w, out, d.out_cap, 0, Lc, nullptr);
+        if (lane == 0) a.sub_res[sn] = make_int2(ovf ? -1 : Lc, after);
+        epoch = pr.epoch;
+        lepoch = pr.lepoch;
+        __syncthreads();
+    }
+    if (lane == 0) atomicMax(a.slot_epoch, epoch);
+}
+
+// k_align_finish: the deferred jobs' B = good regions of A + the better of
+// each bad region and its re-alignment, then realing_end and remove_gaps
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_finish(SaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
+    const int lane = threadIdx.x;
+    SlotEnv e = slot_env(a, lds_u64);
+    uint32_t epoch = next_epoch(a), lepoch = 0;
+    const unsigned int n_fin = a.counters[1];
+    while (true) {
+        unsigned int fn = 0;
+        if (lane == 0) fn = atomicAdd(&a.counters[2], 1u);
+        fn = __shfl(fn, 0);
+        if (fn >= n_fin) break;
+        const int j = a.fin[fn];
+        const SaJob job = a.jobs[j];
+        const int n = job.n, cap = job.cap;
+        WaveCtx w;
+        w.lane = lane;
+        w.n = n;
+        w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+        w.act = lane < n;
+        char* A = (char*)(a.scratch + job.scratch);
+        char* B = A + (size_t)n * cap;
+        char* C = B + (size_t)n * cap;
+        const int R = a.job_nreg[j];
+        const int4* jr = a.job_regions + job.reg_off;
+        int colB = 0;
+        bool ovf = false;
+        for (int ri = 0; ri < R && !ovf; ri++) {
+            const int4 rg = jr[ri];
+            const int len = rg.y - rg.x + 1;
+            if (rg.z > 0) {
+                if (colB + len > cap) {
+                    ovf = true;
+                    break;
+                }
+                cm_copy(w, A, B, cap, rg.x, colB, len);
+                colB += len;
+                continue;
+            }
+            const int sub = -rg.z - 1;
+            const int2 res = a.sub_res[sub];
+            if (res.x < 0) {
+                ovf = true;
+                break;
+            }
+            if (res.y > rg.w) {  // the re-alignment has more identical columns: keep it (reversed back)
+                if (colB + res.x > cap) {
+                    ovf = true;
+                    break;
+                }
+                const SaSub d = a.subs[sub];
+                const char* out = (const char*)(a.pool + d.out_off + 256);
+                for (int r = 0; r < n; r++)
+                    for (int c = lane; c < res.x; c += 64)
+                        B[(size_t)r * cap + colB + c] = out[(size_t)r * d.out_cap + res.x - 1 - c];
+                __syncthreads();
+                colB += res.x;
+            } else {
+                if (colB + len > cap) {
+                    ovf = true;
+                    break;
+                }
+                cm_copy(w, A, B, cap, rg.x, colB, len);
+                colB += len;
+            }
+        }
+        Proc pr(w, a.P, e.S, B, cap, epoch, lepoch);
+        const int L = finish_tail(pr, w, B, C, cap, colB, e.stage, a.stage_bytes, a.P.ac, ovf);
+        if (lane == 0) {
+            a.job_len[j] = ovf ? 0 : L;
+            a.job_status[j] = ovf ? 1 : 0;
+        }
+        epoch = pr.epoch;
+        lepoch = pr.lepoch;
+        __syncthreads();
+    }
+    if (lane == 0) atomicMax(a.slot_epoch, epoch);
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_jobs(SaArgs a) {
@@ -595,7 +995,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 if (w.act) v0.p = stage + off;
             }
         }
-        bool ovf = false;
+        bool ovf = false, deferred = false;
         int L = 0;
         if (a.aligner_type == 1) {
             // DummyAligner: pad to the longest row
@@ -640,7 +1040,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 t_regions = clock64() - t_reg0;
                 st_regions = R;
                 int colB = 0;
-                if (fast && R == 1 && __shfl(rreg.z, 0)) {  // one good region: the alignment stays in A
+                if (a.defer && L0 >= a.defer && !(fast && R == 1 && __shfl(rreg.z, 0)))
+                    deferred = defer_regions(DeferOut{a.job_regions, a.job_nreg, a.subs, a.alloc, a.counters,
+                                                      a.pool, a.pool_cap, a.max_sub, a.fin},
+                                             n, j, job.reg_off, job.reg_cap, A, C, cap, R, fast, counted, rreg,
+                                             gmask, S.regions, S.good_col);
+                if (deferred) {
+                    L = L0;
+                    R = 0;
+                } else if (fast && R == 1 && __shfl(rreg.z, 0)) {  // one good region: the alignment stays in A
                     B = A;
                     colB = L0;
                     R = 0;
@@ -697,8 +1105,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 // 3. realing_end
                 t_ph[1] = clock64() - t0;
                 t0 = clock64();
-                L = colB;
-                if (!ovf && L >= 2) {
+                if (!deferred) L = colB;
+                if (!deferred && !ovf && L >= 2) {
                     int prefix = L - a.P.ac;
                     if (prefix < 1) prefix = 1;
                     const View tv = stage_segment(w, B, cap, C, stage, a.stage_bytes, prefix, L);
@@ -724,10 +1132,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         __syncthreads();
         // 4. remove pure-gap columns
         const long long t_rg = clock64();
-        if (!ovf) L = remove_pure_gap_cols(w, B, cap, L);
+        if (!ovf && !deferred) L = remove_pure_gap_cols(w, B, cap, L);
         if (lane == 0) {
             a.job_len[j] = ovf ? 0 : L;
-            a.job_status[j] = ovf ? 1 : (B == A ? 2 : 0);  // 2: the rows are in A
+            a.job_status[j] = ovf ? 1 : deferred ? 3 : (B == A ? 2 : 0);  // 2: the rows are in A, 3: deferred
             int64_t* js = a.job_stats + (size_t)j * NPGX_JOB_STATS;
             js[0] = clock64() - t_job;
             js[1] = L;
@@ -808,6 +1216,17 @@ struct npgx_aligner {
     DevBuf<unsigned char> good_col;
     DevBuf<GatherRow> d_gather;
     DevBuf<char> d_out;
+    // deferred fix_bad_regions (first attempt)
+    // NPGX_ALIGN_DEFER=<columns>: alignments at least this long hand their bad
+    // regions to k_align_sub (0: every bad region realigned inside its job)
+    int defer = 1000;
+    DevBuf<int4> d_job_regions;
+    DevBuf<int32_t> d_job_nreg, d_fin;
+    DevBuf<SaSub> d_subs;
+    DevBuf<int2> d_sub_res;
+    DevBuf<unsigned long long> d_alloc;
+    DevBuf<unsigned int> d_counters;
+    DevBuf<unsigned char> d_pool;
     // last result
     std::vector<char> out;
     std::vector<int64_t> out_off;
@@ -839,8 +1258,12 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     std::vector<int32_t> ne_len;
     res.row_ne.assign((size_t)std::max<int64_t>(n_rows, 1), -1);
     std::vector<double> cost(n_jobs);
-    int64_t scratch = 0;
+    int64_t scratch = 0, n_reg = 0, n_sub_max = 0;
     int max_n = 1, max_len = 1, max_cap = 1;
+    const int wf = weight_factor(o.min_identity_x1e4);
+    // after reduce_regions every region but a lone one weighs >= min_length:
+    // at least this many columns wide
+    const int min_width = std::max(1, std::min(o.min_length, (o.min_length + wf - 1) / std::max(wf, 1)));
     for (int32_t j = 0; j < n_jobs; j++) {
         const int64_t r0 = job_row_start[j], r1 = job_row_start[j + 1];
         NPGX_REQUIRE(r1 >= r0, NPGX_ERR_ARG, "job_row_start not monotone");
@@ -868,6 +1291,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         J.cap = (int32_t)((std::max<int64_t>(cap, 1) + 15) & ~15ll);
         J.scratch = scratch;
         scratch += (3ll * n * J.cap + 255) & ~255ll;
+        J.reg_off = n_reg;
+        J.reg_cap = n > 1 ? std::min(J.cap + 1, J.cap / min_width + 2) : 0;
+        J.pad = 0;
+        n_reg += J.reg_cap;
+        n_sub_max += (J.reg_cap + 1) / 2;
         cost[j] = double(n) * double(sum);
         max_n = std::max(max_n, n);
         max_len = std::max(max_len, mx);
@@ -910,7 +1338,6 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     };
     put(al->d_row_off.p, ne_off.data(), ne_off.size() * 8);
     put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
-    const int wf = weight_factor(o.min_identity_x1e4);
     Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
 
     std::vector<int32_t> jlen(n_jobs), jstat(n_jobs);
@@ -996,6 +1423,43 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.good_col = al->good_col.p;
         A.slot_cols = slot_cols;
         A.P = P;
+        const bool defer = attempt == 0 && al->defer > 0 && o.aligner_type == 0 && n_reg > 0 && max_cap >= al->defer;
+        A.defer = defer ? al->defer : 0;
+        if (defer) {
+            al->d_job_regions.grow((size_t)n_reg);
+            al->d_job_nreg.grow(jobs.size());
+            al->d_fin.grow(jobs.size());
+            const int64_t max_sub = n_sub_max;
+            al->d_subs.grow((size_t)max_sub);
+            al->d_sub_res.grow((size_t)max_sub);
+            al->d_alloc.ensure(2);
+            al->d_counters.ensure(4);
+            // sub-job outputs: about what the jobs' own scratch holds
+            al->d_pool.grow((size_t)scratch + (16u << 20));
+            NPGX_HIP(hipMemsetAsync(al->d_alloc.p, 0, 16, st));
+            NPGX_HIP(hipMemsetAsync(al->d_counters.p, 0, 16, st));
+            A.job_regions = al->d_job_regions.p;
+            A.job_nreg = al->d_job_nreg.p;
+            A.subs = al->d_subs.p;
+            A.sub_res = al->d_sub_res.p;
+            A.alloc = al->d_alloc.p;
+            A.counters = al->d_counters.p;
+            A.pool = al->d_pool.p;
+            A.pool_cap = (int64_t)al->d_pool.cap;
+            A.max_sub = max_sub;
+            A.fin = al->d_fin.p;
+        } else {
+            A.job_regions = nullptr;
+            A.job_nreg = nullptr;
+            A.subs = nullptr;
+            A.sub_res = nullptr;
+            A.alloc = nullptr;
+            A.counters = nullptr;
+            A.pool = nullptr;
+            A.pool_cap = 0;
+            A.max_sub = 0;
+            A.fin = nullptr;
+        }
         // LDS: word table (16 B/entry) + the largest job's rows.  A workgroup may
         // take all 160 KiB of a CU's LDS; when the batch has more jobs than
         // workgroups can be resident at that size the stage shrinks, and the
@@ -1034,6 +1498,16 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
+        if (defer) {  // the deferred bad regions, then their jobs (both no-ops when nothing was deferred)
+            ti = al->timer.begin("align_sub", st, 0.0, 0);
+            hipLaunchKernelGGL(k_align_sub, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+            NPGX_HIP(hipGetLastError());
+            al->timer.end(ti, st);
+            ti = al->timer.begin("align_finish", st, 0.0, 0);
+            hipLaunchKernelGGL(k_align_finish, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+            NPGX_HIP(hipGetLastError());
+            al->timer.end(ti, st);
+        }
         int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);
         NPGX_HIP(hipMemcpyAsync(pl, al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipMemcpyAsync(pl + n_jobs, al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
@@ -1051,6 +1525,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->pinned.reset();
         std::vector<int32_t> again;
         for (int32_t j : todo) {
+            NPGX_REQUIRE(jstat[j] >= 0 && jstat[j] <= 2, NPGX_ERR_STATE, "alignment job left unfinished");
             if (jstat[j] == 1) {
                 again.push_back(j);
                 continue;
@@ -1182,12 +1657,18 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         a->device = dev;
         const char* js = getenv("NPGX_JOB_STATS");
         a->want_stats = js && js[0] == '1';
+        const char* df = getenv("NPGX_ALIGN_DEFER");
+        if (df && *df) a->defer = std::max(0, atoi(df));
         if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
             delete a;
             throw Error(NPGX_ERR_HIP, "stream creation failed");
         }
-        if (hipFuncSetAttribute((const void*)k_align_jobs, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)LDS_PER_CU) != hipSuccess) {
+        const void* kernels[3] = {(const void*)k_align_jobs, (const void*)k_align_sub, (const void*)k_align_finish};
+        bool lds_ok = true;
+        for (const void* k : kernels)
+            lds_ok = lds_ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) ==
+                                   hipSuccess;
+        if (!lds_ok) {
             (void)hipStreamDestroy(a->stream);
             delete a;
             throw Error(NPGX_ERR_HIP, "cannot enable 160 KiB of LDS for the aligner");

@@ -114,8 +114,29 @@ def test_random_families(seed):
     _check(_random_jobs(seed, 150))
 
 
-def test_long_flanks():
+# NPGX_ALIGN_DEFER (read when the aligner is created): the column count from
+# which fix_bad_regions' re-alignments leave the job's workgroup and run as
+# sub-jobs of their own (0: never, 1: every alignment)
+@pytest.mark.parametrize("defer", ["0", "1", "1000"])
+def test_long_flanks(defer, monkeypatch):
+    monkeypatch.setenv("NPGX_ALIGN_DEFER", defer)
     _check(_random_jobs(11, 40, nmax=17, lmax=1500))
+
+
+@pytest.mark.parametrize("defer", ["0", "1000"])
+def test_very_long_rows(defer, monkeypatch):
+    """Alignments of thousands of columns with hundreds of low-similarity
+    regions (the LDS region reduction and its block minima) and some rows
+    unrelated from part-way."""
+    monkeypatch.setenv("NPGX_ALIGN_DEFER", defer)
+    rng = np.random.default_rng(21)
+    jobs = []
+    for _ in range(12):
+        n = int(rng.integers(2, 18))
+        L = int(rng.integers(4000, 12000))
+        d = float(rng.choice([0.02, 0.05, 0.1]))
+        jobs.append(_family(rng, n, L, d, tail_unrelated=float(rng.choice([0.0, 0.3]))))
+    _check(jobs)
 
 
 def test_wide_blocks():

@@ -36,7 +36,13 @@ for rep in range(5):
         for k, v in st["ms_stage"].items():
             best["ms_stage"][k] = min(best["ms_stage"][k], v)
 st = dict(st, ms_stage_min=best["ms_stage"])
-print(json.dumps({"config": cfg, "wall_ms": round(dt * 1e3, 2), "stats": st}, default=str))
+kt = {}
+for k in eng.kernel_times():  # last rep, summed per kernel (HIP events)
+    e = kt.setdefault(k["name"], [0.0, 0])
+    e[0] += k["ms"]
+    e[1] += 1
+kt = {n: [round(v[0], 3), v[1]] for n, v in sorted(kt.items(), key=lambda x: -x[1][0])}
+print(json.dumps({"config": cfg, "wall_ms": round(dt * 1e3, 2), "stats": st, "kernels": kt}, default=str))
 js = eng.job_stats()
 os.makedirs("gpurun_out", exist_ok=True)
 np.save("gpurun_out/jobstats_%s%s.npy" % (cfg, "_prof" if os.environ.get("NPGX_PROFILE") == "1" else ""), js)

@@ -36,8 +36,11 @@ for rep in range(5):
         for k, v in st["ms_stage"].items():
             best["ms_stage"][k] = min(best["ms_stage"][k], v)
 st = dict(st, ms_stage_min=best["ms_stage"])
+kts = eng.kernel_times()
+print("aligner launches (ms):", [(k["name"][6:], round(k["ms"], 3)) for k in kts if k["name"].startswith("align")],
+      file=sys.stderr)
 kt = {}
-for k in eng.kernel_times():  # last rep, summed per kernel (HIP events)
+for k in kts:  # last rep, summed per kernel (HIP events)
     e = kt.setdefault(k["name"], [0.0, 0])
     e[0] += k["ms"]
     e[1] += 1

@@ -50,9 +50,11 @@ struct Params {
 struct Slot {
     unsigned long long* tkeys;  // try_aligned word table: (epoch << 48 | word)
     unsigned long long* tmask;  // row masks
+    uint32_t* tdone;            // row-parallel search: the word's last first sighting
     uint32_t tcap_log2;
     unsigned long long* lkeys;  // the same table in LDS (tried first)
     unsigned long long* lmask;
+    uint32_t* ldone;
     uint32_t ltab_log2;
     unsigned long long* lwords;  // LDS [row][64]: one chunk's words (vector try_aligned);
                                  // more rows: [shift][64] words of the first HIST_SHIFTS shifts
@@ -68,6 +70,7 @@ struct Slot {
 
 static constexpr int VEC_ROWS = 8;
 typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // LDS-qualified word-table entry
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
 static constexpr int HIST_SHIFTS = 32;  // words per lane kept for the first-sighting scan  // try_aligned with lanes = shifts up to this many rows
 
 struct WaveCtx {
@@ -612,18 +615,24 @@ struct Proc {
             if (r.found) my_shift = r.my_shift;
             return r.found != 0;
         }
-        const int r = find_word<LdsU64>(my_shift, max_shift, (LdsU64*)S.lkeys, (LdsU64*)S.lmask, S.ltab_log2, lepoch,
-                                1 << (S.ltab_log2 - 1));
+        const int r = find_word<LdsU64, LdsU32>(my_shift, max_shift, (LdsU64*)S.lkeys, (LdsU64*)S.lmask,
+                                                (LdsU32*)S.ldone, S.ltab_log2, lepoch, 1 << (S.ltab_log2 - 1));
         if (r >= 0) return r == 1;
-        return find_word<unsigned long long>(my_shift, max_shift, S.tkeys, S.tmask, S.tcap_log2, epoch,
-                                             0x7fffffff) == 1;
+        return find_word<unsigned long long, uint32_t>(my_shift, max_shift, S.tkeys, S.tmask, S.tdone,
+                                                       S.tcap_log2, epoch, 0x7fffffff) == 1;
     }
 
     // 1: found (my_shift set), 0: no shift works, -1: more than `limit` inserts
     // T = unsigned long long (global table) or LdsU64 (the LDS table: ds_* atomics)
-    template <class T>
-    __device__ __forceinline__ int find_word(int& my_shift, int max_shift, T* tkeys, T* tmask, uint32_t tlog,
-                                             uint32_t& ep_ref, int limit) {
+    // Rows in parallel, J = 64/n shifts per step: lane = j*n + r holds row r's
+    // word at shift s0+j.  Per word the table keeps the rows that have had it
+    // (mask) and the largest first-sighting shift (done): at shift s the word
+    // is complete iff mask is full and done <= s, which is what the reference
+    // sees after inserting the words of shifts 0..s.  A row's first sighting
+    // within a step is its lowest j with the word (shuffle compares).
+    template <class T, class U>
+    __device__ __forceinline__ int find_word(int& my_shift, int max_shift, T* tkeys, T* tmask, U* tdone,
+                                             uint32_t tlog, uint32_t& ep_ref, int limit) {
         uint32_t ep32 = ep_ref + 1;
         const uint32_t tcap = 1u << tlog;
         if (ep32 >= 0xFFFF) {  // epoch wrap: clear the table
@@ -636,31 +645,52 @@ struct Proc {
         }
         ep_ref = ep32;
         const unsigned long long ep = (unsigned long long)ep32 << 48;
-        const unsigned long long wmask = (P.ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * P.ac)) - 1);
-        // this call's words of the first HIST_SHIFTS shifts, [shift][lane] in LDS:
+        const int ac = P.ac;
+        const unsigned long long wmask = (ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * ac)) - 1);
+        const int n = w.n;
+        // a step inserts up to 64 keys: keep them well inside the table
+        const int J = tcap >= 256 ? 64 / n : 1;
+        const int r = w.lane % n, j = w.lane / n;
+        const bool act = j < J;
+        const View vr{shfl_ptr(v.p, r), __shfl(v.len, r), __shfl(v.d, r)};
+        const int pr = __shfl(pos, r);
+        // this call's words of the first HIST_SHIFTS shifts, [shift][row] in LDS:
         // the first sighting of the chosen word is then a scan of LDS
         LdsU64* hw = (LdsU64*)S.lwords;
         const bool keep = S.hist_cap > 0;
         unsigned long long word = 0;
-        if (w.act) {
+        int nxt = pr + j + ac - 1;  // next char of this lane's word
+        if (act) {
             int c[15];
 #pragma unroll
-            for (int j = 0; j < 15; j++) c[j] = j < P.ac - 1 ? ch(pos + j) : 0;  // independent loads
+            for (int t = 0; t < 15; t++) c[t] = t < ac - 1 ? vch(vr, pr + j + t, r) : 0;  // independent loads
 #pragma unroll
-            for (int j = 0; j < 15; j++)
-                if (j < P.ac - 1) word = (word << 3) | code3(c[j]);
+            for (int t = 0; t < 15; t++)
+                if (t < ac - 1) word = (word << 3) | code3(c[t]);
         }
         int inserted = 0;
-        for (int s = 0; s < max_shift; s++) {
-            n_shifts++;
-            if (w.act) word = ((word << 3) | code3(ch(pos + s + P.ac - 1))) & wmask;
-            if (keep && s < HIST_SHIFTS) hw[s * 64 + w.lane] = word;
-            // every row inserts its own word: claim (or find) the key, reset
-            // the row mask of a new key, then OR the row bits in
+        for (int s0 = 0; s0 < max_shift; s0 += J) {
+            const int s = s0 + j;
+            const bool valid = act && s < max_shift;
+            const int add = s0 == 0 ? 1 : J;  // chars entering this lane's word
+            if (act) {
+                int c[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) c[t] = t < add ? vch(vr, nxt + t, r) : 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++)
+                    if (t < add) word = (word << 3) | code3(c[t]);
+                word &= wmask;
+                for (int t = 8; t < add; t++) word = ((word << 3) | code3(vch(vr, nxt + t, r))) & wmask;
+                nxt += add;
+            }
+            if (keep && valid && s < HIST_SHIFTS) hw[s * 64 + r] = word;
+            // every lane inserts its word: claim (or find) the key, reset the
+            // row mask and done of a new key, then record first sightings
             const unsigned long long key = ep | word;
             uint32_t slot = 0;
             bool claimed = false;
-            if (w.act) {
+            if (valid) {
                 slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tlog));
                 while (true) {
                     unsigned long long k = __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -671,40 +701,60 @@ struct Proc {
                             claimed = true;
                             break;
                         }
-                        if (k == key) break;  // another row claimed the same word
+                        if (k == key) break;  // another lane claimed the same word
                         continue;
                     }
                     slot = (slot + 1) & (tcap - 1);
                 }
             }
-            if (claimed) __hip_atomic_store(&tmask[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (claimed) {
+                __hip_atomic_store(&tmask[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&tdone[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            bool first = valid;  // the row's lowest j with this word in this step
+            for (int jj = 1; jj < J; jj++) {
+                const unsigned long long o = shfl64(word, max(w.lane - jj * n, 0));
+                if (jj <= j && o == word) first = false;
+            }
             __syncthreads();
-            if (w.act)
-                __hip_atomic_fetch_or(&tmask[slot], 1ull << w.lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (first) {
+                const unsigned long long old =
+                    __hip_atomic_fetch_or(&tmask[slot], 1ull << r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!((old >> r) & 1ull))
+                    __hip_atomic_fetch_max(&tdone[slot], (uint32_t)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             __syncthreads();
-            const unsigned long long m =
-                w.act ? __hip_atomic_load(&tmask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+            bool complete = false;
+            if (valid)
+                complete = __hip_atomic_load(&tmask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == w.rowmask &&
+                           (int)__hip_atomic_load(&tdone[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= s;
             inserted += __popcll(ballot(claimed));
-            const unsigned long long cm = ballot(w.act && m == w.rowmask) & w.rowmask;
+            const unsigned long long cm = ballot(complete);
+            n_shifts += min(J, max_shift - s0);
             if (cm) {
-                const int bl = 63 - __clzll((long long)cm);
-                const unsigned long long best = shfl64(word, bl);
-                if ((ballot(w.act && word == shfl64(word, 0)) & w.rowmask) == w.rowmask) {  // words.size() == 1
-                    my_shift = s;
+                // the first complete shift (lowest j), its highest complete row names the word
+                const int jm = (__ffsll((long long)cm) - 1) / n;
+                const unsigned long long rows = (cm >> (jm * n)) & w.rowmask;
+                const int rb = 63 - __clzll((long long)rows);
+                const unsigned long long best = shfl64(word, jm * n + rb);
+                const int sb = s0 + jm;
+                const unsigned long long same = ballot(act && j == jm && word == shfl64(word, jm * n));
+                if (((same >> (jm * n)) & w.rowmask) == w.rowmask) {  // words.size() == 1
+                    my_shift = sb;
                 } else {
                     my_shift = -1;
                     if (w.act) {
-                        if (keep && s < HIST_SHIFTS) {
-                            for (int t = 0; t <= s; t++)
+                        if (keep && sb < HIST_SHIFTS) {
+                            for (int t = 0; t <= sb; t++)
                                 if (hw[t * 64 + w.lane] == best) {
                                     my_shift = t;
                                     break;
                                 }
                         } else {
                             unsigned long long x = 0;
-                            for (int j = 0; j < P.ac - 1; j++) x = (x << 3) | code3(ch(pos + j));
-                            for (int t = 0; t <= s; t++) {
-                                x = ((x << 3) | code3(ch(pos + t + P.ac - 1))) & wmask;
+                            for (int q = 0; q < ac - 1; q++) x = (x << 3) | code3(ch(pos + q));
+                            for (int t = 0; t <= sb; t++) {
+                                x = ((x << 3) | code3(ch(pos + t + ac - 1))) & wmask;
                                 if (x == best) {
                                     my_shift = t;
                                     break;

@@ -68,6 +68,7 @@ struct SaArgs {
     // per-slot scratch
     unsigned long long* tkeys;
     unsigned long long* tmask;
+    uint32_t* tdone;           // row-parallel search: completion shift of a word
     uint32_t tcap_log2;
     uint32_t* slot_epoch;      // out: highest word-table epoch reached (one word)
     uint32_t epoch_base;       // every slot's first epoch
@@ -707,16 +708,18 @@ __device__ __forceinline__ SlotEnv slot_env(const SaArgs& a, unsigned long long*
     const uint32_t ltab = 1u << a.ltab_log2;
     S.lkeys = lds_u64;
     S.lmask = lds_u64 + ltab;
+    S.ldone = (uint32_t*)(lds_u64 + 2 * ltab);
     S.ltab_log2 = a.ltab_log2;
-    S.lwords = lds_u64 + 2 * ltab;
+    S.lwords = lds_u64 + 2 * ltab + (ltab + 1) / 2;
     S.hist_cap = a.hist_cap;
     for (uint32_t i = lane; i < ltab; i += 64) lds_u64[i] = 0ull;
     __syncthreads();
-    e.stage = (char*)(lds_u64 + 2 * ltab) + a.words_bytes;
+    e.stage = (char*)S.lwords + a.words_bytes;
     const size_t slot = blockIdx.x;
     const size_t tcap = (size_t)1 << a.tcap_log2;
     S.tkeys = a.tkeys + slot * tcap;
     S.tmask = a.tmask + slot * tcap;
+    S.tdone = a.tdone + slot * tcap;
     S.tcap_log2 = a.tcap_log2;
     const size_t stn = (size_t)a.st_depth_max * 64;
     S.st_p = a.st_p + slot * stn;
@@ -902,33 +905,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_jobs(SaArgs a) {
-    extern __shared__ unsigned long long lds_u64[];
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
-    Slot S;
-    const uint32_t ltab = 1u << a.ltab_log2;
-    S.lkeys = lds_u64;
-    S.lmask = lds_u64 + ltab;
-    S.ltab_log2 = a.ltab_log2;
-    S.lwords = lds_u64 + 2 * ltab;
-    S.hist_cap = a.hist_cap;
-    for (uint32_t i = lane; i < ltab; i += 64) lds_u64[i] = 0ull;
-    __syncthreads();
-    char* stage = (char*)(lds_u64 + 2 * ltab) + a.words_bytes;
+    SlotEnv e = slot_env(a, lds_u64);
+    Slot& S = e.S;
+    char* stage = e.stage;
     uint32_t lepoch = 0;
-    const size_t slot = blockIdx.x;
-    const size_t tcap = (size_t)1 << a.tcap_log2;
-    S.tkeys = a.tkeys + slot * tcap;
-    S.tmask = a.tmask + slot * tcap;
-    S.tcap_log2 = a.tcap_log2;
     uint32_t epoch = a.epoch_base;
-    const size_t stn = (size_t)a.st_depth_max * 64;
-    S.st_p = a.st_p + slot * stn;
-    S.st_len = a.st_len + slot * stn;
-    S.st_pos = a.st_pos + slot * stn;
-    S.st_col = a.st_col + slot * a.st_depth_max;
-    S.st_depth_max = a.st_depth_max;
-    S.regions = a.regions + slot * (size_t)a.slot_cols;
-    S.good_col = a.good_col + slot * (size_t)a.slot_cols;
 
     while (true) {
         unsigned int jn = 0;
@@ -1207,6 +1190,7 @@ struct npgx_aligner {
     double host_ms[2] = {0, 0};  // align_device: host preparation, kernel wait
     PinnedArena pinned;          // staging of the batch's host<->device copies
     DevBuf<unsigned long long> tkeys, tmask;
+    DevBuf<uint32_t> tdone;
     DevBuf<uint32_t> slot_epoch;
     size_t tcap_alloc = 0;
     uint32_t epoch_base = 1;  // first word-table epoch of the next launch
@@ -1381,6 +1365,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         if (slots * tcap > al->tcap_alloc || al->epoch_base > 0xF000) {
             al->tkeys.ensure(slots * tcap);
             al->tmask.ensure(slots * tcap);
+            al->tdone.ensure(slots * tcap);  // reset when a key is claimed
             NPGX_HIP(hipMemsetAsync(al->tkeys.p, 0, al->tkeys.cap * 8, st));
             NPGX_HIP(hipMemsetAsync(al->tmask.p, 0, al->tmask.cap * 8, st));  // epoch-tagged masks (vector search)
             al->tcap_alloc = std::max(al->tcap_alloc, slots * tcap);
@@ -1411,6 +1396,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.next_job = al->d_next.p;
         A.tkeys = al->tkeys.p;
         A.tmask = al->tmask.p;
+        A.tdone = al->tdone.p;
         A.tcap_log2 = tlog;
         A.slot_epoch = al->slot_epoch.p;
         A.epoch_base = al->epoch_base;
@@ -1460,7 +1446,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A.max_sub = 0;
             A.fin = nullptr;
         }
-        // LDS: word table (16 B/entry) + the largest job's rows.  A workgroup may
+        // LDS: word table (20 B/entry) + the largest job's rows.  A workgroup may
         // take all 160 KiB of a CU's LDS; when the batch has more jobs than
         // workgroups can be resident at that size the stage shrinks, and the
         // jobs that no longer fit read their rows from global memory.
@@ -1484,8 +1470,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.words_bytes = (int32_t)words_bytes;
         A.ltab_log2 = 0;
         if (max_n > VEC_ROWS)
-            while (A.ltab_log2 < 12 && (16ll << (A.ltab_log2 + 1)) <= (budget - words_bytes) / 2) A.ltab_log2++;
-        const int table_bytes = (int)((16ll << A.ltab_log2) + words_bytes);
+            while (A.ltab_log2 < 12 && (20ll << (A.ltab_log2 + 1)) <= (budget - words_bytes) / 2) A.ltab_log2++;
+        // key, row mask and completion shift per entry
+        const int64_t ltab = 1ll << A.ltab_log2;
+        const int table_bytes = (int)(16 * ltab + 8 * ((ltab + 1) / 2) + words_bytes);
         const int64_t stage_cap = std::max<int64_t>(0, budget - table_bytes);
         A.stage_bytes = o.aligner_type == 0 ? (int32_t)std::min<int64_t>((max_rows + 15) & ~15ll, stage_cap & ~15ll) : 0;
         const size_t lds_bytes = (size_t)table_bytes + (size_t)A.stage_bytes;

@@ -57,8 +57,8 @@ struct Slot {
     uint32_t* ldone;
     uint32_t ltab_log2;
     unsigned long long* lwords;  // LDS [row][64]: one chunk's words (vector try_aligned);
-                                 // more rows: [shift][64] words of the first HIST_SHIFTS shifts
-    int hist_cap;                // > 0: lwords holds HIST_SHIFTS x 64 words
+                                 // more rows: [shift][row] words of the first 2048/n shifts
+    int hist_cap;                // > 0: lwords holds HIST_SHIFTS x 64 words of history
     const char** st_p;          // append_aligned stack, 64 lanes per level
     int* st_len;
     int* st_pos;
@@ -654,10 +654,10 @@ struct Proc {
         const bool act = j < J;
         const View vr{shfl_ptr(v.p, r), __shfl(v.len, r), __shfl(v.d, r)};
         const int pr = __shfl(pos, r);
-        // this call's words of the first HIST_SHIFTS shifts, [shift][row] in LDS:
+        // this call's words of the first `hist` shifts, [shift][row] in LDS:
         // the first sighting of the chosen word is then a scan of LDS
         LdsU64* hw = (LdsU64*)S.lwords;
-        const bool keep = S.hist_cap > 0;
+        const int hist = S.hist_cap > 0 ? S.hist_cap * 64 / n : 0;
         unsigned long long word = 0;
         int nxt = pr + j + ac - 1;  // next char of this lane's word
         if (act) {
@@ -684,7 +684,7 @@ struct Proc {
                 for (int t = 8; t < add; t++) word = ((word << 3) | code3(vch(vr, nxt + t, r))) & wmask;
                 nxt += add;
             }
-            if (keep && valid && s < HIST_SHIFTS) hw[s * 64 + r] = word;
+            if (valid && s < hist) hw[s * n + r] = word;
             // every lane inserts its word: claim (or find) the key, reset the
             // row mask and done of a new key, then record first sightings
             const unsigned long long key = ep | word;
@@ -743,24 +743,42 @@ struct Proc {
                     my_shift = sb;
                 } else {
                     my_shift = -1;
-                    if (w.act) {
-                        if (keep && sb < HIST_SHIFTS) {
+                    if (sb < hist) {
+                        if (w.act)
                             for (int t = 0; t <= sb; t++)
-                                if (hw[t * 64 + w.lane] == best) {
+                                if (hw[t * n + w.lane] == best) {
                                     my_shift = t;
                                     break;
                                 }
-                        } else {
-                            unsigned long long x = 0;
-                            for (int q = 0; q < ac - 1; q++) x = (x << 3) | code3(ch(pos + q));
-                            for (int t = 0; t <= sb; t++) {
-                                x = ((x << 3) | code3(ch(pos + t + ac - 1))) & wmask;
-                                if (x == best) {
-                                    my_shift = t;
-                                    break;
-                                }
+                    } else {
+                        // rescan the rows J shifts per step in the same lane layout
+                        unsigned long long x = 0;
+                        if (act)
+                            for (int q = 0; q < ac - 1; q++) x = (x << 3) | code3(vch(vr, pr + j + q, r));
+                        int at = pr + j + ac - 1, fs = -1;
+                        unsigned long long found = 0;  // rows with a first sighting
+                        for (int t0 = 0; t0 <= sb && (found & w.rowmask) != w.rowmask; t0 += J) {
+                            const int add = t0 == 0 ? 1 : J;
+                            if (act)
+                                for (int t = 0; t < add; t++) x = ((x << 3) | code3(vch(vr, at + t, r))) & wmask;
+                            at += add;
+                            const bool hit = act && t0 + j <= sb && x == best;
+                            const unsigned long long hm = ballot(hit);
+                            // lowest j of each row not found before
+                            if (hit && fs < 0 && !((found >> r) & 1ull)) {
+                                bool lowest = true;
+                                for (int jj = 1; jj <= j; jj++) lowest &= !((hm >> (w.lane - jj * n)) & 1ull);
+                                if (lowest) fs = t0 + j;
                             }
+                            for (int q = 0; q < J; q++) found |= (hm >> (q * n)) & w.rowmask;
                         }
+                        // lane r of the Proc layout takes row r's shift from lane (r, j)
+                        int got = -1;
+                        for (int q = 0; q < J; q++) {
+                            const int o = __shfl(fs, q * n + (w.lane < n ? w.lane : 0));
+                            if (got < 0 && o >= 0) got = o;
+                        }
+                        if (w.act) my_shift = got;
                     }
                 }
                 return 1;

@@ -88,7 +88,7 @@ __device__ __forceinline__ int vch(const View& v, int q, int lane) {
 }
 
 __device__ __forceinline__ bool all_eq(const WaveCtx& w, int c) {
-    const int c0 = __shfl(c, 0);
+    const int c0 = __builtin_amdgcn_readlane(c, 0);
     return (ballot(!w.act || c == c0) & w.rowmask) == w.rowmask;
 }
 
@@ -96,20 +96,27 @@ __device__ __forceinline__ bool any_lane(const WaveCtx& w, bool b) {
     return (ballot(w.act && b) & w.rowmask) != 0;
 }
 
+// Wave reductions with DPP row shifts and row broadcasts (a few VALU cycles
+// each) instead of ds_bpermute round trips; every lane gets the result.
+// Called with all 64 lanes active.
+template <class Op>
+__device__ __forceinline__ int dpp_reduce(int v, int id, Op op) {
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
 __device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return v;
+    return dpp_reduce(v, (int)0x80000000, [](int a, int b) { return max(a, b); });
 }
 __device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return v;
+    return dpp_reduce(v, 0x7fffffff, [](int a, int b) { return min(a, b); });
 }
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    return dpp_reduce(v, 0, [](int a, int b) { return a + b; });
 }
 __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
     const unsigned lo = (unsigned)__shfl((int)(unsigned)v, src);
@@ -118,6 +125,16 @@ __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int s
 }
 __device__ __forceinline__ const char* shfl_ptr(const char* p, int src) {
     return (const char*)shfl64((unsigned long long)p, src);
+}
+// lane k's value for a wave-uniform k: v_readlane instead of ds_bpermute
+__device__ __forceinline__ int bcast(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ unsigned long long bcast64(unsigned long long v, int k) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, k);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), k);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ const char* bcast_ptr(const char* p, int k) {
+    return (const char*)bcast64((unsigned long long)p, k);
 }
 
 // number of trailing one bits
@@ -207,7 +224,7 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
     max_shift = __builtin_amdgcn_readfirstlane(max_shift);
     tcap_log2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)tcap_log2);
     epoch = (uint32_t)__builtin_amdgcn_readfirstlane((int)epoch);
-    W = (unsigned long long*)shfl_ptr((const char*)W, 0);
+    W = (unsigned long long*)bcast_ptr((const char*)W, 0);
     VecOut out{};
     out.epoch = epoch;
     const View v{vp, vlen, vd};
@@ -227,9 +244,9 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
 #endif
         for (int k = 0; k < n; k++) {
             // codes of chars q0 .. q0+127 (two coalesced loads), words by shuffles
-            const char* pk = shfl_ptr(v.p, k);
-            const int lk = __shfl(v.len, k), dk = __shfl(v.d, k);
-            const int q0 = __shfl(pos, k) + S0;
+            const char* pk = bcast_ptr(v.p, k);
+            const int lk = bcast(v.len, k), dk = bcast(v.d, k);
+            const int q0 = bcast(pos, k) + S0;
             const int qa = q0 + lane, qb = q0 + 64 + lane;
             const int ca = qa < lk ? (int)Proc_code3((unsigned char)pk[(ptrdiff_t)dk * qa]) : 6;
             const int cb = qb < lk ? (int)Proc_code3((unsigned char)pk[(ptrdiff_t)dk * qb]) : 6;
@@ -439,8 +456,8 @@ struct Proc {
         }
         __syncthreads();
         for (int r = 0; r < w.n; r++) {
-            const char* pr = shfl_ptr(v.p, r);
-            const int dr = __shfl(v.d, r), qr = __shfl(pos, r), tr = __shfl(t, r);
+            const char* pr = bcast_ptr(v.p, r);
+            const int dr = bcast(v.d, r), qr = bcast(pos, r), tr = bcast(t, r);
             char* o = ob + (size_t)r * cap + col;
             for (int j = w.lane; j < m; j += 64) o[j] = j < tr ? pr[(ptrdiff_t)dr * (qr + j)] : '-';
         }
@@ -465,15 +482,15 @@ struct Proc {
             unsigned long long em, vm;
             {
                 const int j = w.lane;
-                const char* p0 = shfl_ptr(v.p, 0);
-                const int d0 = __shfl(v.d, 0), l0 = __shfl(v.len, 0), q0 = __shfl(pos, 0);
+                const char* p0 = bcast_ptr(v.p, 0);
+                const int d0 = bcast(v.d, 0), l0 = bcast(v.len, 0), q0 = bcast(pos, 0);
                 bool valid = q0 + j < l0;
                 const char c0 = valid ? p0[(ptrdiff_t)d0 * (q0 + j)] : 0;
                 ob[col + j] = c0;  // speculative: columns past the consumed ones are rewritten later
                 bool eq = true;
                 for (int r = 1; r < w.n; r++) {
-                    const char* pr = shfl_ptr(v.p, r);
-                    const int dr = __shfl(v.d, r), lr = __shfl(v.len, r), qr = __shfl(pos, r);
+                    const char* pr = bcast_ptr(v.p, r);
+                    const int dr = bcast(v.d, r), lr = bcast(v.len, r), qr = bcast(pos, r);
                     const bool vr = qr + j < lr;
                     const char c = vr ? pr[(ptrdiff_t)dr * (qr + j)] : 0;
                     ob[(size_t)r * cap + col + j] = c;
@@ -736,9 +753,9 @@ struct Proc {
                 const int jm = (__ffsll((long long)cm) - 1) / n;
                 const unsigned long long rows = (cm >> (jm * n)) & w.rowmask;
                 const int rb = 63 - __clzll((long long)rows);
-                const unsigned long long best = shfl64(word, jm * n + rb);
+                const unsigned long long best = bcast64(word, jm * n + rb);
                 const int sb = s0 + jm;
-                const unsigned long long same = ballot(act && j == jm && word == shfl64(word, jm * n));
+                const unsigned long long same = ballot(act && j == jm && word == bcast64(word, jm * n));
                 if (((same >> (jm * n)) & w.rowmask) == w.rowmask) {  // words.size() == 1
                     my_shift = sb;
                 } else {
@@ -795,14 +812,14 @@ struct Proc {
         int t = 0;
         while (true) {
             const int j = w.lane;
-            const char* p0 = shfl_ptr(v.p, 0);
-            const int d0 = __shfl(v.d, 0), q0 = __shfl(pos, 0), l0 = __shfl(v.len, 0);
+            const char* p0 = bcast_ptr(v.p, 0);
+            const int d0 = bcast(v.d, 0), q0 = bcast(pos, 0), l0 = bcast(v.len, 0);
             const int cp0 = l0 - 1 - (t + j);
             const int c0 = cp0 >= 0 ? (unsigned char)p0[(ptrdiff_t)d0 * cp0] : -1;
             bool E = true, V = q0 < cp0;
             for (int r = 1; r < w.n; r++) {
-                const char* pr = shfl_ptr(v.p, r);
-                const int dr = __shfl(v.d, r), lr = __shfl(v.len, r), qr = __shfl(pos, r);
+                const char* pr = bcast_ptr(v.p, r);
+                const int dr = bcast(v.d, r), lr = bcast(v.len, r), qr = bcast(pos, r);
                 const int cp = lr - 1 - (t + j);
                 const int c = cp >= 0 ? (unsigned char)pr[(ptrdiff_t)dr * cp] : -2;
                 E &= c == c0;
@@ -914,7 +931,7 @@ struct Proc {
             depth--;
             const int child_len = v.len;  // = this row's shift in the parent
             const size_t o = (size_t)depth * 64 + w.lane;
-            const int c0 = __shfl(S.st_col[depth], 0);
+            const int c0 = bcast(S.st_col[depth], 0);
             v.p = S.st_p[o];
             const int l = S.st_len[o];
             v.len = l & 0x7fffffff;

@@ -285,7 +285,7 @@ __device__ int regions_in_registers(const WaveCtx& w, const char* A, int cap, in
         const int t = __shfl_up(pre, o);
         if (lane >= o) pre += t;
     }
-    const int R = __shfl(pre, 63);
+    const int R = bcast(pre, 63);
     if (R > 64) return -1;
     int idx = pre - cnt;
     for (unsigned long long m = starts; m; m &= m - 1) tmp[idx++] = lane * 64 + __ffsll((long long)m) - 1;
@@ -301,9 +301,9 @@ __device__ int regions_in_registers(const WaveCtx& w, const char* A, int cap, in
         const int bw = wave_min(wv);
         if (bw >= min_length) break;
         const int mi = __ffsll((long long)ballot(lane < n && rg.w == bw)) - 1;  // first minimum
-        int4 nr = make_int4(__shfl(rg.x, mi), __shfl(rg.y, mi), __shfl(rg.z, mi), __shfl(rg.w, mi));
-        const int px = __shfl(rg.x, mi > 0 ? mi - 1 : 0), pw = __shfl(rg.w, mi > 0 ? mi - 1 : 0);
-        const int qy = __shfl(rg.y, mi + 1 < 64 ? mi + 1 : 63), qw = __shfl(rg.w, mi + 1 < 64 ? mi + 1 : 63);
+        int4 nr = make_int4(bcast(rg.x, mi), bcast(rg.y, mi), bcast(rg.z, mi), bcast(rg.w, mi));
+        const int px = bcast(rg.x, mi > 0 ? mi - 1 : 0), pw = bcast(rg.w, mi > 0 ? mi - 1 : 0);
+        const int qy = bcast(rg.y, mi + 1 < 64 ? mi + 1 : 63), qw = bcast(rg.w, mi + 1 < 64 ? mi + 1 : 63);
         int first = mi, last = mi;
         if (mi > 0) {
             nr.x = px;
@@ -404,7 +404,7 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
             rw[i] = (int)((gm[q] >> (j & 63)) & 1ull) << 31;  // good flag; weight below
             i++;
         }
-        k += __shfl(pre, 63);
+        k += bcast(pre, 63);
     }
     __syncthreads();
     for (int i = lane; i < R0; i += 64) {
@@ -474,7 +474,7 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
 #pragma unroll
             for (int k = 3; k >= 0; k--) {
                 const unsigned long long m = ballot(bm[k] == bw);
-                if (m) mi = __shfl(bi[k], __ffsll((long long)m) - 1);
+                if (m) mi = bcast(bi[k], __ffsll((long long)m) - 1);
             }
             int hp, hq, p, q;
             merge(mi, hp, hq, p, q);
@@ -627,8 +627,8 @@ __device__ __forceinline__ bool defer_regions(const DeferOut a, int n, int j, in
     int nbad = 0;
     int64_t need = 0;
     for (int ri = 0; ri < R; ri++) {
-        const int4 rg = fast ? make_int4(__shfl(rreg.x, ri), __shfl(rreg.y, ri), __shfl(rreg.z, ri),
-                                         __shfl(rreg.w, ri))
+        const int4 rg = fast ? make_int4(bcast(rreg.x, ri), bcast(rreg.y, ri), bcast(rreg.z, ri),
+                                         bcast(rreg.w, ri))
                              : regions[ri];
         int before = 0;
         if (!rg.z) {
@@ -656,8 +656,8 @@ __device__ __forceinline__ bool defer_regions(const DeferOut a, int n, int j, in
         base = reserve(&a.alloc[0], (unsigned long long)need, (unsigned long long)a.pool_cap);
         if (base >= 0) s0 = (long long)atomicAdd(&a.alloc[1], (unsigned long long)nbad);  // max_sub bounds every job's bad regions
     }
-    base = (long long)shfl64((unsigned long long)base, 0);
-    s0 = (long long)shfl64((unsigned long long)s0, 0);
+    base = (long long)bcast64((unsigned long long)base, 0);
+    s0 = (long long)bcast64((unsigned long long)s0, 0);
     __syncthreads();
     if (base < 0) return false;
     int64_t off = base;
@@ -737,14 +737,14 @@ __device__ __forceinline__ void stage_rows(View& v0, int n, char* stage, int sta
     const int lane = threadIdx.x;
     int off = 0, tot = 0;
     for (int r = 0; r < n; r++) {
-        const int lr = __shfl(v0.len, r);
+        const int lr = bcast(v0.len, r);
         if (lane == r) off = tot;
         tot += lr;
     }
     if (tot > stage_bytes) return;
     for (int r = 0; r < n; r++) {
-        const char* src = shfl_ptr(v0.p, r);
-        const int lr = __shfl(v0.len, r), o = __shfl(off, r);
+        const char* src = bcast_ptr(v0.p, r);
+        const int lr = bcast(v0.len, r), o = bcast(off, r);
         for (int base = 0; base < lr; base += 64 * 8) {
             char x[8];
 #pragma unroll
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     while (true) {
         unsigned int sn = 0;
         if (lane == 0) sn = atomicAdd(&a.counters[0], 1u);
-        sn = __shfl(sn, 0);
+        sn = bcast(sn, 0);
         if (sn >= n_sub) break;
         const SaSub d = a.subs[sn];
         const SaJob job = a.jobs[d.job];
@@ -835,7 +835,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     while (true) {
         unsigned int fn = 0;
         if (lane == 0) fn = atomicAdd(&a.counters[2], 1u);
-        fn = __shfl(fn, 0);
+        fn = bcast(fn, 0);
         if (fn >= n_fin) break;
         const int j = a.fin[fn];
         const SaJob job = a.jobs[j];
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     while (true) {
         unsigned int jn = 0;
         if (lane == 0) jn = atomicAdd(a.next_job, 1u);
-        jn = __shfl(jn, 0);
+        jn = bcast(jn, 0);
         if (jn >= (unsigned)a.n_jobs) break;
         const int j = a.order[jn];
         const SaJob job = a.jobs[j];
@@ -952,14 +952,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             // is then an LDS read instead of a global one
             int off = 0, tot = 0;
             for (int r = 0; r < n; r++) {
-                const int lr = __shfl(v0.len, r);
+                const int lr = bcast(v0.len, r);
                 if (lane == r) off = tot;
                 tot += lr;
             }
             if (tot <= a.stage_bytes) {
                 for (int r = 0; r < n; r++) {
-                    const char* src = shfl_ptr(v0.p, r);
-                    const int lr = __shfl(v0.len, r), o = __shfl(off, r);
+                    const char* src = bcast_ptr(v0.p, r);
+                    const int lr = bcast(v0.len, r), o = bcast(off, r);
                     for (int base = 0; base < lr; base += 64 * 8) {
                         char x[8];
 #pragma unroll
@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 t_regions = clock64() - t_reg0;
                 st_regions = R;
                 int colB = 0;
-                if (a.defer && L0 >= a.defer && !(fast && R == 1 && __shfl(rreg.z, 0)))
+                if (a.defer && L0 >= a.defer && !(fast && R == 1 && bcast(rreg.z, 0)))
                     deferred = defer_regions(DeferOut{a.job_regions, a.job_nreg, a.subs, a.alloc, a.counters,
                                                       a.pool, a.pool_cap, a.max_sub, a.fin},
                                              n, j, job.reg_off, job.reg_cap, A, C, cap, R, fast, counted, rreg,
@@ -1031,15 +1031,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 if (deferred) {
                     L = L0;
                     R = 0;
-                } else if (fast && R == 1 && __shfl(rreg.z, 0)) {  // one good region: the alignment stays in A
+                } else if (fast && R == 1 && bcast(rreg.z, 0)) {  // one good region: the alignment stays in A
                     B = A;
                     colB = L0;
                     R = 0;
                 }
                 pr.ob = B;
                 for (int ri = 0; ri < R && !ovf; ri++) {
-                    const int4 rg = fast ? make_int4(__shfl(rreg.x, ri), __shfl(rreg.y, ri), __shfl(rreg.z, ri),
-                                                     __shfl(rreg.w, ri))
+                    const int4 rg = fast ? make_int4(bcast(rreg.x, ri), bcast(rreg.y, ri), bcast(rreg.z, ri),
+                                                     bcast(rreg.w, ri))
                                          : S.regions[ri];
                     const int len = rg.y - rg.x + 1;
                     if (colB + len > cap) {

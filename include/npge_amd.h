@@ -126,6 +126,45 @@ int npgx_af_clear_used(npgx_af* af);
 int npgx_af_kernel_times(const npgx_af* af, npgx_kernel_time* out, int32_t cap, int32_t* n);
 void npgx_af_free(npgx_af* af);
 
+/* ------------------------------------------------------------------ multi-GPU
+ * Exact sharding of ONE AnchorFinder run over `world` ranks (one process per
+ * GPU).  The windows of the run are split into contiguous
+ * ranges, one per rank; the result equals npgx_af_run on one GPU bit for bit.
+ * The exchange steps go through caller-supplied collectives (the host binds
+ * them to torch.distributed -- RCCL over xGMI on MI355X, gloo in tests):
+ *   1. the Bloom first-setter array: element-wise MIN over ranks (the
+ *      reference's sequential "bits set by an earlier window", BloomFilter.cpp
+ *      :65-76, AnchorFinder.cpp:170-197, is a MIN of window orders per bit);
+ *   2. the collected hashes (bloomtg_postprocess :213-218): all-gather;
+ *   3. FoundFragment counts per hash (truncation :356-391): SUM;
+ *   4. the FoundFragment keys of the kept groups: all-gather.
+ * Every rank ends with the whole result and the same used-hash set.
+ * Callbacks return 0 on success; buffers named dev live in device memory of
+ * the handle's device, the library's stream is idle when a callback runs, and
+ * the callback must have finished its writes when it returns.  Every rank
+ * must call npgx_af_run_sharded with the same inputs and options. */
+#define NPGX_OP_SUM 0
+#define NPGX_OP_MIN 1
+typedef struct {
+    int32_t rank;
+    int32_t world;
+    void* user;
+    /* in-place element-wise reduction of n int32 values (op NPGX_OP_SUM/MIN) */
+    int (*allreduce_i32)(void* user, int32_t* dev, int64_t n, int32_t op);
+    /* out[r] = value of rank r (host memory, world entries) */
+    int (*allgather_i64)(void* user, int64_t value, int64_t* out);
+    /* concatenation in rank order of counts[r] uint64 values from each rank
+     * into dev_out (capacity sum(counts)); counts is host memory */
+    int (*allgatherv_u64)(void* user, const uint64_t* dev_in, const int64_t* counts,
+                          uint64_t* dev_out);
+} npgx_comm;
+
+int npgx_af_run_sharded(npgx_af* af, const npgx_seqset* s, const npgx_comm* comm);
+
+/* Copies bytes between any two of host/device memory (hipMemcpyDefault);
+ * for host-side collective adapters. */
+int npgx_memcpy(void* dst, const void* src, int64_t bytes);
+
 /* ------------------------------------------------------------------ aligner
  * Batched AbstractAligner::align_seqs with aligner-type "similar"
  * (SimilarAligner) or "dummy" (DummyAligner).  A batch holds n_jobs independent

@@ -97,6 +97,8 @@ def lib():
     L.npgx_af_kernel_times.argtypes = [vp, P(KernelTime), i32, P(i32)]
     L.npgx_af_free.argtypes = [vp]
     L.npgx_af_free.restype = None
+    L.npgx_af_run_sharded.argtypes = [vp, vp, vp]
+    L.npgx_memcpy.argtypes = [vp, vp, i64]
     if hasattr(L, "npgx_aligner_create"):
         L.npgx_align_default_options.argtypes = [P(AlignOptions)]
         L.npgx_align_default_options.restype = None

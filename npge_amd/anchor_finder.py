@@ -78,6 +78,18 @@ class AnchorFinder(Processor):
         _capi.check(L.npgx_af_run(h, seqset.handle))
         return self.result()
 
+    def find_sharded(self, seqset, comm):
+        """Exactly sharded run over the ranks of `comm` (npge_amd.comm.TorchComm):
+        this rank scans its window range; the result on every rank equals
+        find() on one GPU."""
+        L = _capi.lib()
+        h = self._handle()
+        rc = L.npgx_af_run_sharded(h, seqset.handle, comm.pointer())
+        if rc != 0 and comm.errors:
+            raise _capi.NpgxError(rc, "; ".join(comm.errors))
+        _capi.check(rc)
+        return self.result()
+
     def result(self):
         L = _capi.lib()
         h = self._h

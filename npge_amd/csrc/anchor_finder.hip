@@ -280,6 +280,21 @@ __global__ __launch_bounds__(WG) void k_ff_scatter(AfArgs a, TableArgs t, const 
     cand[slot] = ((uint64_t)idx << key_bits) | key2;
 }
 
+// uint32 <-> order-preserving int32 (x ^ 2^31), so a signed MIN collective over
+// ranks is the unsigned MIN of first-setter orders (0xFFFFFFFF = "never set").
+__global__ void k_flip_sign(uint32_t* __restrict__ v, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] ^= 0x80000000u;
+}
+
+// this rank's candidates in the kept groups: local offset of group G
+__global__ void k_local_cut(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ counts,
+                            int64_t nH, uint64_t G, uint64_t* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    out[3] = G < (uint64_t)nH ? (uint64_t)offsets[G]
+                              : (nH ? (uint64_t)offsets[nH - 1] + counts[nH - 1] : 0ull);
+}
+
 // ------------------------------------------------------------------ host helpers
 static int bits_for(uint64_t v) {  // bits needed to represent values < v
     int b = 0;
@@ -306,6 +321,8 @@ struct npgx_af {
     DevBuf<unsigned long long> counters;  // [0] = n_raw, [1] = n_unique
     DevBuf<uint64_t> tkeys;
     DevBuf<uint32_t> tvals, counts, offsets, cursor;
+    DevBuf<uint32_t> counts_local, offsets_local;  // sharded runs: this rank's windows
+    DevBuf<uint64_t> gathered;                     // sharded runs: all ranks' hashes / keys
     DevBuf<uint64_t> cut;  // G, C, total
     DevBuf<uint64_t> cand, cand_sorted;
     DevBuf<unsigned char> temp;
@@ -391,7 +408,11 @@ void glibc_rand(uint32_t seed, int n, uint64_t* out) {
     for (int i = 0; i < n; i++) out[i] = (uint64_t)(r[344 + (size_t)i] >> 1);
 }
 
-static void af_run(npgx_af* af, const npgx_seqset* ss) {
+static void comm_check(int rc, const char* what) {
+    if (rc != 0) throw Error(NPGX_ERR_ARG, std::string("collective callback failed: ") + what);
+}
+
+static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     NPGX_REQUIRE(ss->device == af->device, NPGX_ERR_ARG, "sequence set and finder on different devices");
     NPGX_HIP(hipSetDevice(af->device));
     hipStream_t st = af->stream;
@@ -450,8 +471,18 @@ static void af_run(npgx_af* af, const npgx_seqset* ss) {
                                     hipMemcpyHostToDevice, st));
         af->used_dirty = false;
     }
-    const int64_t nchunks = (int64_t)chunks.size();
-    if (nchunks == 0) {
+    const int64_t nchunks_all = (int64_t)chunks.size();
+    // sharded run: this rank scans the contiguous chunk range [c0, c1)
+    const int world = comm ? comm->world : 1;
+    const int rank = comm ? comm->rank : 0;
+    const int64_t c0 = nchunks_all * rank / world, c1 = nchunks_all * (rank + 1) / world;
+    const int64_t nchunks = c1 - c0;
+    if (comm) NPGX_REQUIRE(n_windows < (1ll << 31), NPGX_ERR_RANGE,
+                           "sharded run: FoundFragment counts must fit int32");
+    int64_t local_windows = 0;
+    for (int64_t c = c0; c < c1; c++)
+        local_windows += std::min<int64_t>(WG, meta[chunks[c].seq].size - k + 1 - chunks[c].pos);
+    if (nchunks_all == 0) {
         af->r_block_start.assign(1, 0);
         af->r_seq.clear();
         af->r_min.clear();
@@ -468,7 +499,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss) {
                             hipMemcpyHostToDevice, st));
 
     A.meta = af->d_meta.p;
-    A.chunks = af->d_chunks.p;
+    A.chunks = af->d_chunks.p + c0;
     A.words = ss->words.p;
     A.nmask = ss->nmask.p;
     A.used = af->d_used.p;
@@ -481,23 +512,37 @@ static void af_run(npgx_af* af, const npgx_seqset* ss) {
     A.mmagic = ~0ull / (uint64_t)m;
     A.similar = af->opt.anchor_similar ? 1 : 0;
 
-    const dim3 grid((unsigned)nchunks), block(WG);
+    const dim3 grid((unsigned)std::max<int64_t>(nchunks, 1)), block(WG);
+    const bool run_local = nchunks > 0;  // ranks without windows still join every collective
     uint64_t* hp = af->h_pinned;
 
     // --- pass 1: Bloom first-setter + found/collect
     af->first.ensure((size_t)m);
     af->counters.ensure(4);
     NPGX_HIP(hipMemsetAsync(af->counters.p, 0, 4 * sizeof(unsigned long long), st));
-    size_t ti = af->timer.begin("bloom_first", st, n_windows * (0.375 + 8.0 * kb), n_windows);
+    size_t ti = af->timer.begin("bloom_first", st, local_windows * (0.375 + 8.0 * kb), local_windows);
     NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
-    hipLaunchKernelGGL(k_bloom_first, grid, block, 0, st, A, af->first.p);
+    if (run_local) hipLaunchKernelGGL(k_bloom_first, grid, block, 0, st, A, af->first.p);
     NPGX_HIP(hipGetLastError());
     af->timer.end(ti, st);
+    if (comm) {
+        // exchange 1: first[bit] = MIN over ranks (windows of every rank)
+        const dim3 fg((unsigned)((m + 255) / 256));
+        ti = af->timer.begin("first_allreduce", st, (double)m * 4 * 2, m);
+        hipLaunchKernelGGL(k_flip_sign, fg, dim3(256), 0, st, af->first.p, (int64_t)m);
+        NPGX_HIP(hipStreamSynchronize(st));
+        comm_check(comm->allreduce_i32(comm->user, (int32_t*)af->first.p, m, NPGX_OP_MIN),
+                   "allreduce(first, MIN)");
+        hipLaunchKernelGGL(k_flip_sign, fg, dim3(256), 0, st, af->first.p, (int64_t)m);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
+    }
 
-    af->hraw.ensure((size_t)n_windows);
-    ti = af->timer.begin("found_collect", st, n_windows * (0.375 + 4.0 * kb), n_windows);
-    hipLaunchKernelGGL(k_found_collect, grid, block, 0, st, A, af->first.p, af->hraw.p,
-                       af->counters.p);
+    af->hraw.ensure((size_t)std::max<int64_t>(local_windows, 1));
+    ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
+    if (run_local)
+        hipLaunchKernelGGL(k_found_collect, grid, block, 0, st, A, af->first.p, af->hraw.p,
+                           af->counters.p);
     NPGX_HIP(hipGetLastError());
     af->timer.end(ti, st);
     NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8, hipMemcpyDeviceToHost, st));
@@ -506,26 +551,41 @@ static void af_run(npgx_af* af, const npgx_seqset* ss) {
     S.n_collected_raw = n_raw;
 
     // --- bloomtg_postprocess (AnchorFinder.cpp:213-218): sort + unique
-    int64_t nH = 0;
-    if (n_raw > 0) {
-        af->hsorted.ensure((size_t)n_raw);
-        af->huniq.ensure((size_t)n_raw);
+    const unsigned h_end_bit = (unsigned)std::min(64, 2 * k);
+    auto sort_unique = [&](const uint64_t* in, int64_t n) -> int64_t {
+        if (n <= 0) return 0;
+        af->hsorted.ensure((size_t)n);
+        af->huniq.ensure((size_t)n);
         size_t b1 = 0, b2 = 0;
-        const unsigned end_bit = (unsigned)std::min(64, 2 * k);
-        NPGX_HIP(rocprim::radix_sort_keys(nullptr, b1, af->hraw.p, af->hsorted.p, (size_t)n_raw, 0u,
-                                          end_bit, st));
+        NPGX_HIP(rocprim::radix_sort_keys(nullptr, b1, in, af->hsorted.p, (size_t)n, 0u, h_end_bit, st));
         NPGX_HIP(rocprim::unique(nullptr, b2, af->hsorted.p, af->huniq.p, af->counters.p + 1,
-                                 (size_t)n_raw, rocprim::equal_to<uint64_t>(), st));
+                                 (size_t)n, rocprim::equal_to<uint64_t>(), st));
         af->ensure_temp(std::max(b1, b2));
-        ti = af->timer.begin("sort_unique_H", st, n_raw * 8.0 * 4, n_raw);
-        NPGX_HIP(rocprim::radix_sort_keys(af->temp.p, b1, af->hraw.p, af->hsorted.p, (size_t)n_raw,
-                                          0u, end_bit, st));
+        size_t t = af->timer.begin("sort_unique_H", st, n * 8.0 * 4, n);
+        NPGX_HIP(rocprim::radix_sort_keys(af->temp.p, b1, in, af->hsorted.p, (size_t)n, 0u, h_end_bit, st));
         NPGX_HIP(rocprim::unique(af->temp.p, b2, af->hsorted.p, af->huniq.p, af->counters.p + 1,
-                                 (size_t)n_raw, rocprim::equal_to<uint64_t>(), st));
-        af->timer.end(ti, st);
+                                 (size_t)n, rocprim::equal_to<uint64_t>(), st));
+        af->timer.end(t, st);
         NPGX_HIP(hipMemcpyAsync(hp, af->counters.p + 1, 8, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipStreamSynchronize(st));
-        nH = (int64_t)hp[0];
+        return (int64_t)hp[0];
+    };
+    std::vector<int64_t> rc(world);
+    // all-gather of this rank's n values from `src` into af->gathered; returns the total
+    auto gather_u64 = [&](const uint64_t* src, int64_t n, const char* what) -> int64_t {
+        comm_check(comm->allgather_i64(comm->user, n, rc.data()), what);
+        int64_t tot = 0;
+        for (int64_t v : rc) tot += v;
+        af->gathered.grow((size_t)std::max<int64_t>(tot, 1));
+        NPGX_HIP(hipStreamSynchronize(st));
+        if (tot > 0) comm_check(comm->allgatherv_u64(comm->user, src, rc.data(), af->gathered.p), what);
+        return tot;
+    };
+    int64_t nH = sort_unique(af->hraw.p, n_raw);
+    if (comm) {
+        // exchange 2: every rank's unique collected hashes -> the global H
+        const int64_t tot = gather_u64(af->huniq.p, nH, "allgatherv(collected hashes)");
+        nH = sort_unique(af->gathered.p, tot);
     }
     S.n_collected = nH;
 
@@ -559,10 +619,20 @@ static void af_run(npgx_af* af, const npgx_seqset* ss) {
         af->cursor.ensure((size_t)nH);
         NPGX_HIP(hipMemsetAsync(af->counts.p, 0, (size_t)nH * 4, st));
         NPGX_HIP(hipMemsetAsync(af->cursor.p, 0, (size_t)nH * 4, st));
-        ti = af->timer.begin("ff_count", st, n_windows * (0.375 + 12.0), n_windows);
-        hipLaunchKernelGGL(k_ff_count, grid, block, 0, st, A, T, af->counts.p);
+        ti = af->timer.begin("ff_count", st, local_windows * (0.375 + 12.0), local_windows);
+        if (run_local) hipLaunchKernelGGL(k_ff_count, grid, block, 0, st, A, T, af->counts.p);
         NPGX_HIP(hipGetLastError());
         af->timer.end(ti, st);
+        if (comm) {
+            // exchange 3: global FoundFragment count per hash; keep this rank's own
+            af->counts_local.ensure((size_t)nH);
+            af->offsets_local.ensure((size_t)nH);
+            NPGX_HIP(hipMemcpyAsync(af->counts_local.p, af->counts.p, (size_t)nH * 4,
+                                    hipMemcpyDeviceToDevice, st));
+            NPGX_HIP(hipStreamSynchronize(st));
+            comm_check(comm->allreduce_i32(comm->user, (int32_t*)af->counts.p, nH, NPGX_OP_SUM),
+                       "allreduce(counts, SUM)");
+        }
         size_t b3 = 0;
         NPGX_HIP(rocprim::exclusive_scan(nullptr, b3, af->counts.p, af->offsets.p, 0u, (size_t)nH,
                                          rocprim::plus<uint32_t>(), st));
@@ -585,20 +655,42 @@ static void af_run(npgx_af* af, const npgx_seqset* ss) {
             const int idx_bits = bits_for(G);
             NPGX_REQUIRE(idx_bits + key_bits <= 64, NPGX_ERR_RANGE,
                          "FoundFragment sort key does not fit 64 bits");
-            af->cand.ensure(C);
+            // sharded: this rank scatters its own windows by its own offsets
+            uint64_t C_local = C;
+            const uint32_t* scatter_off = af->offsets.p;
+            if (comm) {
+                NPGX_HIP(rocprim::exclusive_scan(af->temp.p, b3, af->counts_local.p, af->offsets_local.p,
+                                                 0u, (size_t)nH, rocprim::plus<uint32_t>(), st));
+                hipLaunchKernelGGL(k_local_cut, dim3(1), dim3(64), 0, st, af->offsets_local.p,
+                                   af->counts_local.p, nH, G, af->cut.p);
+                NPGX_HIP(hipGetLastError());
+                NPGX_HIP(hipMemcpyAsync(hp, af->cut.p + 3, 8, hipMemcpyDeviceToHost, st));
+                NPGX_HIP(hipStreamSynchronize(st));
+                C_local = hp[0];
+                scatter_off = af->offsets_local.p;
+            }
+            af->cand.ensure(std::max<uint64_t>(C_local, 1));
             af->cand_sorted.ensure(C);
-            ti = af->timer.begin("ff_scatter", st, n_windows * 0.375 + C * 24.0, n_windows);
-            hipLaunchKernelGGL(k_ff_scatter, grid, block, 0, st, A, T, af->huniq.p, G, af->offsets.p,
-                               af->cursor.p, key_bits, af->cand.p);
+            ti = af->timer.begin("ff_scatter", st, local_windows * 0.375 + C_local * 24.0, local_windows);
+            if (run_local && C_local > 0)
+                hipLaunchKernelGGL(k_ff_scatter, grid, block, 0, st, A, T, af->huniq.p, G, scatter_off,
+                                   af->cursor.p, key_bits, af->cand.p);
             NPGX_HIP(hipGetLastError());
             af->timer.end(ti, st);
+            const uint64_t* sort_in = af->cand.p;
+            if (comm) {
+                // exchange 4: all ranks' FoundFragment keys of the kept groups
+                const int64_t tot = gather_u64(af->cand.p, (int64_t)C_local, "allgatherv(FoundFragments)");
+                NPGX_REQUIRE((uint64_t)tot == C, NPGX_ERR_STATE, "sharded FoundFragment count mismatch");
+                sort_in = af->gathered.p;
+            }
             size_t b4 = 0;
             const unsigned end_bit = (unsigned)(idx_bits + key_bits);
-            NPGX_HIP(rocprim::radix_sort_keys(nullptr, b4, af->cand.p, af->cand_sorted.p, (size_t)C, 0u,
+            NPGX_HIP(rocprim::radix_sort_keys(nullptr, b4, sort_in, af->cand_sorted.p, (size_t)C, 0u,
                                               end_bit, st));
             af->ensure_temp(b4);
             ti = af->timer.begin("ff_sort", st, C * 32.0, (int64_t)C);
-            NPGX_HIP(rocprim::radix_sort_keys(af->temp.p, b4, af->cand.p, af->cand_sorted.p, (size_t)C,
+            NPGX_HIP(rocprim::radix_sort_keys(af->temp.p, b4, sort_in, af->cand_sorted.p, (size_t)C,
                                               0u, end_bit, st));
             af->timer.end(ti, st);
             const uint64_t keep = std::min<uint64_t>(C, (uint64_t)af->opt.max_anchor_fragments);
@@ -699,7 +791,18 @@ int npgx_af_create(const npgx_af_options* o, npgx_af** out) {
 int npgx_af_run(npgx_af* af, const npgx_seqset* s) {
     return guard([&] {
         NPGX_REQUIRE(af && s, NPGX_ERR_ARG, "null argument");
-        af_run(af, s);
+        af_run(af, s, nullptr);
+    });
+}
+
+int npgx_af_run_sharded(npgx_af* af, const npgx_seqset* s, const npgx_comm* comm) {
+    return guard([&] {
+        NPGX_REQUIRE(af && s && comm, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(comm->world >= 1 && comm->rank >= 0 && comm->rank < comm->world, NPGX_ERR_ARG,
+                     "bad rank / world");
+        NPGX_REQUIRE(comm->allreduce_i32 && comm->allgather_i64 && comm->allgatherv_u64, NPGX_ERR_ARG,
+                     "missing collective callback");
+        af_run(af, s, comm->world > 1 ? comm : nullptr);
     });
 }
 

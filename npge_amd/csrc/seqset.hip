@@ -172,6 +172,13 @@ int npgx_set_device(int32_t device) {
     return guard([&] { NPGX_HIP(hipSetDevice(device)); });
 }
 
+int npgx_memcpy(void* dst, const void* src, int64_t bytes) {
+    return guard([&] {
+        NPGX_REQUIRE(bytes >= 0 && (bytes == 0 || (dst && src)), NPGX_ERR_ARG, "npgx_memcpy: bad arguments");
+        if (bytes) NPGX_HIP(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault));
+    });
+}
+
 int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char* const* names,
                        int32_t n, npgx_seqset** out) {
     return guard([&] {

@@ -1,0 +1,90 @@
+"""Exactly sharded AnchorFinder (npgx_af_run_sharded) on the GPU:
+2 and 3 ranks (processes) share the box's one MI355X, exchanging over gloo with
+host staging (RCCL cannot put two ranks on one GPU; the product path binds
+the same callbacks to RCCL).  Every rank's result -- SoA anchors, |H|,
+FoundFragment count, the persistent used-hash set over two runs -- must equal
+the single-GPU npgx_af_run bit for bit, including truncation by
+max-anchor-fragments and anchor-similar=false."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("block_start", "seq", "min_pos", "max_pos", "ori")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _af(maxf, similar):
+    from npge_amd.anchor_finder import AnchorFinder
+    p = AnchorFinder()
+    p.set_opt_value("max-anchor-fragments", maxf)
+    p.set_opt_value("anchor-similar", similar)
+    return p
+
+
+def _pack(r, used):
+    d = {k: np.asarray(r[k]) for k in KEYS}
+    d.update(n_collected=r["n_collected"], n_found_frags=r["n_found_frags"], used=used)
+    return d
+
+
+def _worker(rank, world, port, config, maxf, similar, out):
+    import torch.distributed as dist
+    from npge_amd import _capi, synth
+    from npge_amd.comm import TorchComm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _capi.check(_capi.lib().npgx_set_device(0))
+    names, seqs = synth.genome_set(config)
+    ss = _capi.SeqSet(seqs, names)
+    comm = TorchComm(dist, staging="cpu")
+    sh = _af(maxf, similar)
+    res = []
+    for _ in range(2):  # second run: the persistent used-hash set is in play
+        r = sh.find_sharded(ss, comm)
+        res.append(_pack(r, sh.used_hashes()))
+    ref = None
+    if rank == 0:
+        one = _af(maxf, similar)
+        ref = []
+        for _ in range(2):
+            r = one.find(ss)
+            ref.append(_pack(r, one.used_hashes()))
+    out[rank] = (res, ref)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,config,maxf,similar", [
+    (2, "small", 100000, True),
+    (3, "small", 5000, True),
+    (2, "tiny", 100000, False),
+])
+def test_sharded_equals_single(world, config, maxf, similar):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), config, maxf, similar, out), nprocs=world,
+             join=True)
+    ref = out[0][1]
+    assert len(ref[0]["seq"]) > 0
+    for r in range(world):
+        res = out[r][0]
+        for run in range(2):
+            a, b = res[run], ref[run]
+            for k in KEYS:
+                np.testing.assert_array_equal(a[k], b[k], err_msg="rank %d run %d %s" % (r, run, k))
+            assert a["n_collected"] == b["n_collected"]
+            assert a["n_found_frags"] == b["n_found_frags"]
+            np.testing.assert_array_equal(a["used"], b["used"])

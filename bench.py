@@ -6,9 +6,13 @@ resident in HBM: AnchorFinder (k=20, fp=0.1, max 100000 fragments) followed by
 the block build on its anchors (DraftPangenome-equivalent).
 value = input bp of all ranks / max-over-ranks wall time of the K timed steps.
 
-Multi-GPU (torch.distributed.run, one rank per GPU over RCCL): every rank
-processes its own genome set (same config, rank-specific seed) -- weak scaling
-with no data-path collective (DESIGN.md "Multi-GPU").
+Multi-GPU (torch.distributed.run, one rank per GPU over RCCL), two modes:
+  --mode replicas (default): every rank processes its own genome set (same
+    config, rank-specific seed) -- weak scaling, no data-path collective;
+  --mode sharded: ONE genome set, the AnchorFinder windows and the aligner jobs
+    split over the ranks with RCCL exchanges (npge_amd/comm.py) -- strong
+    scaling; value = that set's bp / time.
+(DESIGN.md "Multi-GPU").
 
 Prints ONE JSON line on rank 0.
 """
@@ -29,6 +33,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--mode", choices=("replicas", "sharded"), default="replicas")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="C2", help="synthetic config timed for cpu_baseline")
     return ap.parse_args()
@@ -50,18 +55,24 @@ def main():
     from npge_amd import pipeline
 
     _capi.check(_capi.lib().npgx_set_device(local_rank))
-    seed = harness.rank_seed(synth.BASE_SEED, rank, args.config)
+    sharded = args.mode == "sharded" and world > 1
+    seed = harness.rank_seed(synth.BASE_SEED, 0 if sharded else rank, args.config)
     names, seqs = synth.genome_set(args.config, seed=seed)
     bp = synth.total_bp(seqs)
     ss = _capi.SeqSet(seqs, names)          # resident in HBM before timing
-    job = pipeline.BlockBuild(ss, names, seqs)
+    comm = None
+    if sharded:
+        from npge_amd.comm import TorchComm
+        comm = TorchComm(dist, staging="cuda")
+    job = pipeline.BlockBuild(ss, names, seqs, comm=comm)
 
     def step():
         return job.run()
 
     dt, info = harness.timed_steps(step, args.steps, args.warmup, dist if world > 1 else None,
                                    sync=torch.cuda.synchronize, device="cuda")
-    value = harness.throughput(bp, world, args.steps, dt) / 1e6
+    # sharded: the ranks share one set of bp; replicas: each rank has its own
+    value = harness.throughput(bp, 1 if sharded else world, args.steps, dt) / 1e6
 
     # dominant kernel of the last step: algorithmic bytes / HIP-event duration
     # (events recorded on the engine's own stream around each launch)
@@ -95,14 +106,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded Brucella-like proxy, npge_amd/synth.py)",
             "config": {"workload": job.workload_name(args.config), "bp_per_rank": bp,
                        "genomes": synth.CONFIGS[args.config][0], "anchor_size": 20,
                        "anchor_fp": 0.1, "max_anchor_fragments": 100000,
-                       "parallelism": "replica-per-gpu x%d" % world},
+                       "parallelism": ("sharded x%d (RCCL)" % world) if sharded
+                       else "replica-per-gpu x%d" % world},
             "last_step": info,
             "kernels_last_step": kernels,
             "roofline": roofline,

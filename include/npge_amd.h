@@ -267,6 +267,13 @@ int npgx_blockset_set_blocks(npgx_blockset* b, int64_t n_blocks, const int64_t* 
                              const int32_t* seq, const int64_t* min_pos, const int64_t* max_pos,
                              const int8_t* ori, const int64_t* row_off, const char* rows);
 /* append the blocks found by the last npgx_af_run of af */
+/* Multi-GPU block build: with a comm of world > 1, DraftPangenome
+ * runs npgx_af_run_sharded and every FragmentsExtender batch aligns this rank's
+ * share of the jobs (longest-processing-time assignment on rows x residues)
+ * and all-gathers the gapped rows; the rest of the build runs identically on
+ * every rank, so every rank ends with the one-GPU block set.  The comm must
+ * outlive the handle's runs; NULL (or world 1) returns to one GPU. */
+int npgx_blockset_set_comm(npgx_blockset* b, const npgx_comm* comm);
 int npgx_blockset_add_anchors(npgx_blockset* b, const npgx_af* af);
 /* run a processor by its reference name (see above); DraftPangenome uses af */
 int npgx_blockset_apply(npgx_blockset* b, const char* processor, npgx_af* af);

@@ -47,6 +47,7 @@ def _bind(L):
     L.npgx_blockset_create.argtypes = [vp, P(BbOptions), P(vp)]
     L.npgx_blockset_set_blocks.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp]
     L.npgx_blockset_add_anchors.argtypes = [vp, vp]
+    L.npgx_blockset_set_comm.argtypes = [vp, vp]
     L.npgx_blockset_apply.argtypes = [vp, ctypes.c_char_p, vp]
     L.npgx_blockset_counts.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.npgx_blockset_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
@@ -87,6 +88,13 @@ class BlockSetEngine:
         h = ctypes.c_void_p()
         _capi.check(L.npgx_blockset_create(seqset.handle, ctypes.byref(o), ctypes.byref(h)))
         self._h = h
+
+    def set_comm(self, comm):
+        """Shards DraftPangenome / FragmentsExtender over comm's ranks
+        (npge_amd.comm.TorchComm); None returns to one GPU."""
+        self._comm = comm  # the library keeps a pointer to comm.struct
+        _capi.check(_capi.lib().npgx_blockset_set_comm(self._h, comm.pointer() if comm else None))
+        return self
 
     def set_blocks(self, blocks):
         """blocks: list of lists of (seq_index, min, max, ori, row_or_None)."""

@@ -9,10 +9,12 @@ STAGES = ["AnchorFinder", "RemoveNonStem", "DummyAligner", "ExtendLoopFast(10)",
 
 
 class BlockBuild:
-    def __init__(self, seqset, names, seqs, seed=1):
+    def __init__(self, seqset, names, seqs, seed=1, comm=None):
         self.ss = seqset
         self.seed = seed
         self.eng = BlockSetEngine(seqset)
+        if comm is not None:  # one genome set sharded over the ranks of comm
+            self.eng.set_comm(comm)
         self.af = AnchorFinder()
         self.af.set_opt_value("bloom-seed", self.seed)
 

@@ -39,7 +39,7 @@ def _pack(r, used):
     return d
 
 
-def _worker(rank, world, port, config, maxf, similar, out):
+def _worker(rank, world, port, config, maxf, similar, staging, out):
     import torch.distributed as dist
     from npge_amd import _capi, synth
     from npge_amd.comm import TorchComm
@@ -49,7 +49,7 @@ def _worker(rank, world, port, config, maxf, similar, out):
     _capi.check(_capi.lib().npgx_set_device(0))
     names, seqs = synth.genome_set(config)
     ss = _capi.SeqSet(seqs, names)
-    comm = TorchComm(dist, staging="cpu")
+    comm = TorchComm(dist, staging=staging)
     sh = _af(maxf, similar)
     res = []
     for _ in range(2):  # second run: the persistent used-hash set is in play
@@ -67,16 +67,17 @@ def _worker(rank, world, port, config, maxf, similar, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,config,maxf,similar", [
-    (2, "small", 100000, True),
-    (3, "small", 5000, True),
-    (2, "tiny", 100000, False),
+@pytest.mark.parametrize("world,config,maxf,similar,staging", [
+    (2, "small", 100000, True, "cpu"),
+    (3, "small", 5000, True, "cpu"),
+    (2, "tiny", 100000, False, "cpu"),
+    (2, "small", 100000, True, "cuda"),   # device staging tensors (the RCCL adapter's path)
 ])
-def test_sharded_equals_single(world, config, maxf, similar):
+def test_sharded_equals_single(world, config, maxf, similar, staging):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), config, maxf, similar, out), nprocs=world,
-             join=True)
+    mp.spawn(_worker, args=(world, _free_port(), config, maxf, similar, staging, out),
+             nprocs=world, join=True)
     ref = out[0][1]
     assert len(ref[0]["seq"]) > 0
     for r in range(world):
@@ -88,3 +89,44 @@ def test_sharded_equals_single(world, config, maxf, similar):
             assert a["n_collected"] == b["n_collected"]
             assert a["n_found_frags"] == b["n_found_frags"]
             np.testing.assert_array_equal(a["used"], b["used"])
+
+
+def _bb_worker(rank, world, port, config, out):
+    import torch.distributed as dist
+    from npge_amd import _capi, synth
+    from npge_amd.comm import TorchComm
+    from npge_amd.pipeline import BlockBuild
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _capi.check(_capi.lib().npgx_set_device(0))
+    names, seqs = synth.genome_set(config)
+    ss = _capi.SeqSet(seqs, names)
+    comm = TorchComm(dist, staging="cpu")
+    job = BlockBuild(ss, names, seqs, comm=comm)
+    info = job.run()
+    got = (job.eng.hash(), job.eng.blocks(), info["align_jobs"])
+    ref = None
+    if rank == 0:
+        one = BlockBuild(ss, names, seqs)
+        one.run()
+        ref = (one.eng.hash(), one.eng.blocks())
+    out[rank] = (got, ref)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,config", [(2, "small"), (3, "tiny")])
+def test_sharded_draft_pangenome_equals_single(world, config):
+    """DraftPangenome with the AnchorFinder and every FragmentsExtender batch
+    sharded: every rank's block set (fragments and gapped rows) equals one GPU's."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bb_worker, args=(world, _free_port(), config, out), nprocs=world, join=True)
+    ref_hash, ref_blocks = out[0][1]
+    assert len(ref_blocks) > 0
+    for r in range(world):
+        (h, blocks, n_jobs) = out[r][0]
+        assert n_jobs > 0
+        assert h == ref_hash, "rank %d" % r
+        assert blocks == ref_blocks, "rank %d" % r

@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--mode", choices=("replicas", "sharded"), default="replicas")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="C2", help="synthetic config timed for cpu_baseline")
     return ap.parse_args()
@@ -47,9 +49,14 @@ def main():
 
     import torch
     import torch.distributed as dist
+    if args.dist_backend == "gloo":  # rehearsal on fewer GPUs than ranks
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from npge_amd import _capi, harness, synth
     from npge_amd import pipeline
@@ -77,7 +84,9 @@ def main():
     # dominant kernel of the last step: algorithmic bytes / HIP-event duration
     # (events recorded on the engine's own stream around each launch)
     kts = job.kernel_times()
-    dom = max(kts, key=lambda k: k["ms"]) if kts else None
+    # (collective stages of a sharded run are timed too but are not kernels)
+    kern = [k for k in kts if not k["name"].endswith("_allreduce")]
+    dom = max(kern, key=lambda k: k["ms"]) if kern else None
     roofline = None
     if dom and dom["ms"] > 0:
         ach = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9

@@ -292,6 +292,40 @@ int npgx_blockset_kernel_times(const npgx_blockset* b, npgx_kernel_time* out, in
 int npgx_blockset_job_stats(const npgx_blockset* b, int64_t* out, int64_t cap, int64_t* n);
 void npgx_blockset_free(npgx_blockset* b);
 
+/* ------------------------------------------------------------------ banded DP
+ * GeneralAligner (src/util/GeneralAligner.hpp:28-414): banded min-cost
+ * Needleman-Wunsch with gap frame 2*gap_range+1 and the max_errors stop rule
+ * ("find the end of good alignment"), align() then optionally cut_tail() and
+ * export_alignment(), on nucleotide contents: substitution 0 for equal non-N
+ * letters, mismatch_penalty otherwise (FragmentDistance.cpp:18-21).  A batch
+ * of independent pairs per call; one wave per pair on the GPU (anti-diagonal
+ * wavefront).  Defaults = GeneralAligner's constructor (:39-41): gap_range 1,
+ * max_errors 0, gap_penalty 1; mismatch_penalty 1.  gap_range <= 63.  Local
+ * mode (find_aln, used by BSA only) is not provided. */
+typedef struct npgx_dp npgx_dp;
+typedef struct {
+    int32_t gap_range;
+    int32_t max_errors;        /* -1: no limit (the alignment is completed to the last cell) */
+    int32_t gap_penalty;
+    int32_t mismatch_penalty;
+    int32_t cut_tail;          /* strip the bad tail (cut_tail :240-255); needs max_errors >= 0 */
+} npgx_dp_options;
+void npgx_dp_default_options(npgx_dp_options* o);
+int npgx_dp_create(const npgx_dp_options* o, npgx_dp** out);
+/* pair i = first[first_off[i] .. first_off[i+1]) against second[second_off[i] ..) */
+int npgx_dp_align_batch(npgx_dp* dp, const char* first, const int64_t* first_off,
+                        const char* second, const int64_t* second_off, int32_t n_pairs);
+int npgx_dp_result_counts(const npgx_dp* dp, int64_t* n_pairs, int64_t* total_ops);
+/* Per pair: last aligned position in first / second (-1: none), score = at()
+ * of that cell (1000000 = BAD_VALUE for a completed end outside the band),
+ * status (0; -1 "row and column are not last"; -2 empty input), and the
+ * alignment as ops[op_off[i] .. op_off[i+1]) in order: 0 = both letters
+ * (MATCH), 1 = first only (ROW_INC), 2 = second only (COL_INC). */
+int npgx_dp_result_copy(const npgx_dp* dp, int32_t* first_last, int32_t* second_last,
+                        int32_t* score, int32_t* status, int64_t* op_off /* n+1 */, int8_t* ops);
+int npgx_dp_kernel_times(const npgx_dp* dp, npgx_kernel_time* out, int32_t cap, int32_t* n);
+void npgx_dp_free(npgx_dp* dp);
+
 #ifdef __cplusplus
 }
 #endif

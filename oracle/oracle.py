@@ -28,8 +28,9 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or (
-            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "npge_oracle.cpp"))
+        if not os.path.exists(_LIB_PATH) or any(
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, f))
+            for f in ("npge_oracle.cpp", "general_aligner.cpp")
         ):
             build()
         L = ctypes.CDLL(_LIB_PATH)
@@ -63,6 +64,11 @@ def lib():
         L.orc_align.argtypes = [ctypes.c_int, ctypes.c_char_p, vp, vp, ctypes.c_int, vp, i64,
                                 ctypes.POINTER(i64), ctypes.POINTER(i64)]
         L.orc_align.restype = ctypes.c_int
+        P32 = ctypes.POINTER(ctypes.c_int)
+        L.orc_ga_align.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, P32, P32, P32, vp, P32]
+        L.orc_ga_align.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -105,6 +111,42 @@ def optimal_hashes(members, bits):
 
 def weight_factor(min_identity_x1e4):
     return lib().orc_weight_factor(min_identity_x1e4)
+
+
+def general_align(a, b, gap_range, max_errors, gap_penalty=1, mismatch_penalty=1,
+                  cut_tail=False):
+    """GeneralAligner align (+ cut_tail) + export_alignment on nucleotide
+    contents (oracle/general_aligner.cpp).  Returns dict(first_last,
+    second_last, score, ops) with ops 0 = MATCH, 1 = ROW_INC (letter of the
+    first sequence only), 2 = COL_INC (second only); {"status": -1} for the reference's
+    "row and column are not last" exception, {"status": -2} for an empty input."""
+    ab = a.encode() if isinstance(a, str) else a
+    bb = b.encode() if isinstance(b, str) else b
+    ops = np.zeros(len(ab) + len(bb) + 1, dtype=np.int8)
+    fl, sl, sc, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = lib().orc_ga_align(ab, len(ab), bb, len(bb), gap_range, max_errors, gap_penalty,
+                            mismatch_penalty, int(cut_tail), ctypes.byref(fl), ctypes.byref(sl),
+                            ctypes.byref(sc), _ptr(ops), ctypes.byref(n))
+    if rc != 0:
+        return {"status": rc}
+    return dict(status=0, first_last=fl.value, second_last=sl.value, score=sc.value, ops=ops[:n.value].copy())
+
+
+def ops_to_rows(a, b, ops):
+    """Gapped rows of an exported alignment (pairs of positions, -1 = gap)."""
+    ra, rb, i, j = [], [], 0, 0
+    for o in ops:
+        if o in (0, 1):
+            ra.append(a[i])
+            i += 1
+        else:
+            ra.append("-")
+        if o in (0, 2):
+            rb.append(b[j])
+            j += 1
+        else:
+            rb.append("-")
+    return "".join(ra), "".join(rb)
 
 
 def to_atgcn(s):

@@ -324,6 +324,10 @@ int npgx_dp_result_counts(const npgx_dp* dp, int64_t* n_pairs, int64_t* total_op
 int npgx_dp_result_copy(const npgx_dp* dp, int32_t* first_last, int32_t* second_last,
                         int32_t* score, int32_t* status, int64_t* op_off /* n+1 */, int8_t* ops);
 int npgx_dp_kernel_times(const npgx_dp* dp, npgx_kernel_time* out, int32_t cap, int32_t* n);
+/* diagnostic build only (NPGX_PROFILE=1): summed per-wave cycles of the
+ * forward pass and of the traceback, and the anti-diagonal steps, of the
+ * last batch */
+int npgx_dp_phase_cycles(const npgx_dp* dp, int64_t* fwd, int64_t* back, int64_t* steps);
 void npgx_dp_free(npgx_dp* dp);
 
 #ifdef __cplusplus

@@ -29,7 +29,9 @@
 // Scores are exact int32 arithmetic: at(prev) < at(cur) along a traced path is
 // exactly "the step cost is positive", which is what cut_tail needs.
 #include <algorithm>
+#include <climits>
 #include <cstring>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -38,6 +40,11 @@ namespace ga {
 
 static constexpr int BAD_VALUE = 1000000;   // GeneralAligner.hpp:24
 static constexpr int RING = 256;            // open rows (<= gap_range + 2 at a time)
+#ifdef NPGX_SA_PROFILE
+static constexpr int RES = 8;  // + cycles of the forward pass and of the traceback
+#else
+static constexpr int RES = 5;
+#endif
 enum { MATCH = 0, ROW_INC = 1, COL_INC = 2 };
 
 struct Pair {
@@ -69,8 +76,62 @@ __device__ __forceinline__ int sub(const char* a, const char* b, int r, int c, i
     return (x == b[c] && x != 'N') ? 0 : mm;
 }
 
+// wave-wide lane shifts by one (DPP wave_shr:1 / wave_shl:1, gfx9 family);
+// the lane shifted in from outside the wave gets `edge`
+__device__ __forceinline__ int from_lane_below(int v, int edge) {  // lane l gets lane l-1's v
+    return __builtin_amdgcn_update_dpp(edge, v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int from_lane_above(int v, int edge) {  // lane l gets lane l+1's v
+    return __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);
+}
+
+static constexpr int LWIN = 256;  // LDS window of each sequence (bytes, a ring)
+static constexpr int REFILL = 32; // steps per window refill / mismatch-mask batch
+
+// high bit of each byte set iff that byte of x is zero (exact)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+
+// 16 substitution flags (1 = mismatch or N) of the cells (r0+k, c0+k),
+// k < 16, from the LDS windows: dword loads, byte-aligned by v_alignbyte,
+// byte-parallel compares (FragmentDistance.cpp:18-21 semantics)
+__device__ __forceinline__ uint32_t mism16(const uint32_t* wa, const uint32_t* wb, int r0, int c0) {
+    const int ia = r0 >> 2, sa = r0 & 3, ib = c0 >> 2, sb = c0 & 3;
+    uint32_t A[5], B[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        A[i] = wa[(ia + i) & (LWIN / 4 - 1)];
+        B[i] = wb[(ib + i) & (LWIN / 4 - 1)];
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(A[i + 1], A[i], sa);
+        const uint32_t y = __builtin_amdgcn_alignbyte(B[i + 1], B[i], sb);
+        const uint32_t good = zero_bytes(x ^ y) & ~zero_bytes(x ^ 0x4E4E4E4Eu);  // equal, not N
+        const uint32_t bad = (~good >> 7) & 0x01010101u;
+        m |= ((bad * 0x01020408u) >> 24) << (4 * i);
+    }
+    return m;
+}
+
+struct Fwd {  // per-wave state of the forward pass
+    int H0, H1;
+    uint32_t acc;
+    int r_row, r_col, r_score, next_row;
+    bool pend;
+    unsigned long long pend_key;
+    int end_v;
+    int loaded;
+    char pre;
+};
+
 __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
     __shared__ unsigned long long ring[RING];
+    __shared__ uint32_t wa32[LWIN / 4], wb32[LWIN / 4];
+    char* wa = (char*)wa32;
+    char* wb = (char*)wb32;
     const int lane = threadIdx.x;
     const Pair P = A.pairs[blockIdx.x];
     const char* a = A.a + P.a_off;
@@ -79,9 +140,9 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
     const int G = A.gr, gp = A.gp, mm = A.mm;
     const Geo g{P.la, P.lb, G};
     const int max_row = g.max_row();
+    int32_t* out = A.res + (int64_t)blockIdx.x * RES;
     if (P.la == 0 || P.lb == 0) {  // find_aln handles these without the aligner (:612-615)
         if (lane == 0) {
-            int32_t* out = A.res + (int64_t)blockIdx.x * 5;
             out[0] = -1;
             out[1] = -1;
             out[2] = 0;
@@ -91,25 +152,88 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
         return;
     }
     for (int i = lane; i < RING; i += 64) ring[i] = ~0ull;
+    // letters: the first 128 of each sequence, then 32 more per refill from a
+    // register loaded one refill ahead (lanes 0-31: a, lanes 32-63: b)
+    for (int i = lane; i < 128; i += 64) {
+        wa[i] = i < P.la ? a[i] : 0;
+        wb[i] = i < P.lb ? b[i] : 0;
+    }
+    const int pl = lane & 31;
+    Fwd F;
+    F.loaded = 128;
+    F.pre = lane < 32 ? (F.loaded + pl < P.la ? a[F.loaded + pl] : 0) : (F.loaded + pl < P.lb ? b[F.loaded + pl] : 0);
     __syncthreads();
 
     // registers: the last value on each owned diagonal (frame value at start)
     const int q0 = 2 * lane, q1 = 2 * lane + 1;
-    int H0 = q0 <= 2 * G + 1 ? abs(q0 - G) * gp : BAD_VALUE;
-    int H1 = q1 <= 2 * G + 1 ? abs(q1 - G) * gp : BAD_VALUE;
-    int r_row = -1, r_col = -1, r_score = 0;
-    int next_row = 0;
-    uint32_t acc = 0;
+    F.H0 = q0 <= 2 * G + 1 ? abs(q0 - G) * gp : BAD_VALUE;
+    F.H1 = q1 <= 2 * G + 1 ? abs(q1 - G) * gp : BAD_VALUE;
+    F.acc = 0;
+    F.r_row = -1;
+    F.r_col = -1;
+    F.r_score = 0;
+    F.next_row = 0;
+    F.pend = false;
+    F.pend_key = 0;
+    F.end_v = BAD_VALUE;
     const int s_end = max_row >= 0 ? max_row + g.max_col(max_row) : -1;
-    int s = 0;
-    for (; s <= s_end; s++) {
+    const int end_c = max_row >= 0 ? g.max_col(max_row) : -1;
+    const bool stop_rule = A.max_errors != -1;
+
+    // keeps the windows ahead of the steps [s, s + REFILL)
+    auto window = [&](int s) {
+        const int need = (s + REFILL + G + 2) / 2 + 2;
+        bool wrote = false;
+        while (F.loaded < need + 32) {
+            if (lane < 32) wa[(F.loaded + pl) & (LWIN - 1)] = F.pre;
+            else wb[(F.loaded + pl) & (LWIN - 1)] = F.pre;
+            F.loaded += 32;
+            F.pre = lane < 32 ? (F.loaded + pl < P.la ? a[F.loaded + pl] : 0)
+                              : (F.loaded + pl < P.lb ? b[F.loaded + pl] : 0);
+            wrote = true;
+        }
+        if (wrote) __syncthreads();
+    };
+    // stop test of the row completed on the previous step (:144-147); true = stop
+    auto pending = [&]() -> bool {
+        if (!F.pend) return false;
+        F.pend = false;
+        const int best = (int)(F.pend_key >> 32);
+        if (best > A.max_errors) return true;
+        F.r_row = F.next_row - 1;
+        F.r_col = (int)(F.pend_key & 0xFFFFFFFFull);
+        F.r_score = best;
+        return false;
+    };
+    // row minima and the row that completes on step s (rows complete in order,
+    // <= 1 per step); its minimum is tested at the top of the next step
+    auto rows = [&](int s, bool live, int r, int c, int v) {
+        if (live) atomicMin(&ring[r & (RING - 1)], ((unsigned long long)(unsigned)v << 32) | (unsigned)c);
+        if (F.next_row <= max_row && F.next_row + g.max_col(F.next_row) == s) {
+            F.pend_key = ring[F.next_row & (RING - 1)];
+            if (lane == 0) ring[F.next_row & (RING - 1)] = ~0ull;  // LDS ops stay in order
+            F.pend = true;
+            F.next_row++;
+        }
+    };
+    auto put_code = [&](int s, uint32_t code) {
+        F.acc |= code << (2 * (s & 15));
+        if ((s & 15) == 15) {
+            track[(int64_t)(s >> 4) * 64 + lane] = F.acc;
+            F.acc = 0;
+        }
+    };
+
+    // the general step: frame, band edges and matrix ends (the first
+    // gap_range + 2 anti-diagonals and the last ones)
+    auto slow_step = [&](int s) {
         const int p = (s + G) & 1;
         const int q = 2 * lane + p;
         const int d = q - G;
         const int r = (s - d) >> 1, c = (s + d) >> 1;
-        const int up_nb = __shfl_down(H0, 1);   // lane+1's even diagonal = q+1 when p = 1
-        const int left_nb = __shfl_up(H1, 1);   // lane-1's odd diagonal = q-1 when p = 0
-        const int Hd = p ? H1 : H0;
+        const int up_nb = from_lane_above(F.H0, BAD_VALUE);   // q+1 when p = 1
+        const int left_nb = from_lane_below(F.H1, BAD_VALUE); // q-1 when p = 0
+        const int Hd = p ? F.H1 : F.H0;
         int v = Hd;
         uint32_t code = 0;
         bool live = false;
@@ -117,51 +241,119 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
             if (q > 2 * G || r > max_row || c > g.max_col(r)) {
                 v = BAD_VALUE;
             } else {
-                int left = p ? H0 : (lane ? left_nb : (c == 0 ? (r + 1) * gp : BAD_VALUE));
-                int up = p ? (lane < 63 ? up_nb : BAD_VALUE) : H1;
-                const int match = Hd + sub(a, b, r, c, mm);
+                const int left = p ? F.H0 : (lane ? left_nb : (c == 0 ? (r + 1) * gp : BAD_VALUE));
+                const int up = p ? up_nb : F.H1;
+                const char x = wa[r & (LWIN - 1)];
+                const int match = Hd + ((x == wb[c & (LWIN - 1)] && x != 'N') ? 0 : mm);
                 const int gap1 = left + gp;
                 const int gap2 = up + gp;
                 v = min(match, min(gap1, gap2));
                 code = v == match ? MATCH : v == gap1 ? COL_INC : ROW_INC;
                 live = true;
+                if (r == max_row && c == end_c) F.end_v = v;
             }
-            if (p) H1 = v;
-            else H0 = v;
+            if (p) F.H1 = v;
+            else F.H0 = v;
         }
-        acc |= code << (2 * (s & 15));
-        if ((s & 15) == 15) {
-            track[(int64_t)(s >> 4) * 64 + lane] = acc;
-            acc = 0;
-        }
-        if (live) atomicMin(&ring[r & (RING - 1)], ((unsigned long long)(unsigned)v << 32) | (unsigned)c);
-        // the row that completes on this step (rows complete in order, <= 1 per step)
-        if (next_row <= max_row && next_row + g.max_col(next_row) == s) {
-            const unsigned long long key = ring[next_row & (RING - 1)];
-            __syncthreads();  // single wave: orders the read before the reset
-            if (lane == 0) ring[next_row & (RING - 1)] = ~0ull;
-            const int best = (int)(key >> 32);
-            if (A.max_errors != -1 && best > A.max_errors) break;
-            r_row = next_row;
-            r_col = (int)(key & 0xFFFFFFFFull);
-            r_score = best;
-            next_row++;
-        }
+        put_code(s, code);
+        if (stop_rule) rows(s, live, r, c, v);
+    };
+
+    // interior anti-diagonals: every band cell of the step is inside the
+    // matrix and off the frame, so the step is branch-free
+    const int L = min(max_row, min(g.cols - 1, g.side() - 1));
+    const int f0 = G + 2;
+    int f1 = min(s_end + 1, 2 * L - G);
+    f1 = f1 < f0 + 2 ? f0 : f0 + ((f1 - f0) & ~1);  // whole step pairs (or none)
+    const int lo0 = q0 > 2 * G ? BAD_VALUE : INT_MIN;  // out-of-band diagonals stay BAD
+    const int lo1 = q1 > 2 * G ? BAD_VALUE : INT_MIN;
+
+    int s = 0;
+    bool stopped = false;
+#ifdef NPGX_SA_PROFILE
+    const long long t_start = clock64();
+#endif
+    for (; s < min(f0, s_end + 1); s++) {
+        if ((stopped = pending())) break;
+        if ((s & (REFILL - 1)) == 0) window(s);
+        slow_step(s);
     }
-    {  // the last step's 16-step block, unless it was just stored
-        const int last = min(s, s_end);
-        if (last >= 0 && (last & 15) != 15) track[(int64_t)(last >> 4) * 64 + lane] = acc;
+    // pairs (s, s+1): step s on the lane's diagonal qa = 2j + P, step s+1 on
+    // qb = 2j + 1 - P, P = (f0 + gap_range) & 1 for every pair
+    auto fast = [&](auto PC) {
+        constexpr int P = decltype(PC)::value;
+        const int qa = 2 * lane + P, qb = 2 * lane + (1 - P);
+        const int da = qa - G, db = qb - G;
+        const int lo_a = P ? lo1 : lo0, lo_b = P ? lo0 : lo1;
+        int ha = P ? F.H1 : F.H0;
+        int hb = P ? F.H0 : F.H1;
+        uint32_t ma = 0, mb = 0;
+        int k = 16;
+        for (; s < f1; s += 2, k++) {
+            if (k == 16) {  // the next 16 pairs' substitution flags
+                window(s);
+                ma = mism16(wa32, wb32, (s - da) >> 1, (s + da) >> 1);
+                mb = mism16(wa32, wb32, (s + 1 - db) >> 1, (s + 1 + db) >> 1);
+                k = 0;
+            }
+            if (stop_rule && (stopped = pending())) break;
+            {  // step s
+                const int left = P == 0 ? from_lane_below(hb, BAD_VALUE) : hb;
+                const int up = P == 0 ? hb : from_lane_above(hb, BAD_VALUE);
+                const int match = ha + (int)((ma >> k) & 1u) * mm;
+                const int gap1 = left + gp, gap2 = up + gp;
+                const int v = min(match, min(gap1, gap2));
+                put_code(s, v == match ? MATCH : v == gap1 ? COL_INC : ROW_INC);
+                ha = max(v, lo_a);
+                if (stop_rule) rows(s, qa <= 2 * G, (s - da) >> 1, (s + da) >> 1, ha);
+            }
+            if (stop_rule && (stopped = pending())) {
+                s += 1;  // step s is done
+                break;
+            }
+            {  // step s+1
+                const int left = P == 0 ? ha : from_lane_below(ha, BAD_VALUE);
+                const int up = P == 0 ? from_lane_above(ha, BAD_VALUE) : ha;
+                const int match = hb + (int)((mb >> k) & 1u) * mm;
+                const int gap1 = left + gp, gap2 = up + gp;
+                const int v = min(match, min(gap1, gap2));
+                put_code(s + 1, v == match ? MATCH : v == gap1 ? COL_INC : ROW_INC);
+                hb = max(v, lo_b);
+                if (stop_rule) rows(s + 1, qb <= 2 * G, (s + 1 - db) >> 1, (s + 1 + db) >> 1, hb);
+            }
+        }
+        F.H0 = P ? hb : ha;
+        F.H1 = P ? ha : hb;
+    };
+    if (!stopped && s == f0 && f1 > f0) {
+        if ((f0 + G) & 1) fast(std::integral_constant<int, 1>{});
+        else fast(std::integral_constant<int, 0>{});
     }
+    const int s_tail = s;
+    for (; s <= s_end && !stopped; s++) {
+        if ((stopped = pending())) break;
+        if ((s & (REFILL - 1)) == 0 || s == s_tail) window(s);
+        slow_step(s);
+    }
+    if (!stopped && F.pend) pending();  // the last row's test
+    {  // the last computed step's 16-step block, unless it was just stored
+        const int last = s - 1;
+        if (last >= 0 && (last & 15) != 15) track[(int64_t)(last >> 4) * 64 + lane] = F.acc;
+    }
+    int r_row = F.r_row, r_col = F.r_col, r_score = F.r_score;
+    const int end_v = F.end_v;
     __threadfence();
     __syncthreads();
+#ifdef NPGX_SA_PROFILE
+    const long long t_fwd = clock64();
+#endif
 
-    int32_t* out = A.res + (int64_t)blockIdx.x * 5;
     int status = 0;
     int end_row = r_row, end_col = r_col, score = r_score;
     int forced_row = 0, forced_col = 0;  // max_errors == -1 completion (:151-172)
-    if (A.max_errors == -1) {
+    if (!stop_rule) {
         end_row = max_row;
-        end_col = max_row >= 0 ? g.max_col(max_row) : min(g.cols - 1, min(g.side() - 1, G - 1));
+        end_col = end_c;
         const int last_row = g.rows - 1, last_col = g.cols - 1;
         if (end_row == last_row) {
             forced_col = last_col - end_col;
@@ -170,7 +362,11 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
         } else {
             status = -1;  // "row and column are not last"
         }
-        score = 0;
+        // at() of the completion cell: computed in the band, or BAD_VALUE for a
+        // forced end (cells the reference never computes either)
+        score = (forced_row || forced_col || end_row < 0)
+                    ? BAD_VALUE
+                    : __builtin_amdgcn_readlane(end_v, (end_col - end_row + G) >> 1);
     }
     if (status != 0) {
         if (lane == 0) {
@@ -183,47 +379,40 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
         return;
     }
 
-    // traceback reader: one coalesced load per 16-step block, 2 bits by readlane
+    // traceback reader: 16-step blocks of directions, one coalesced load each,
+    // the next two blocks down prefetched; a cell's 2 bits by readlane
     int blk = -1;
-    uint32_t w = 0;
+    uint32_t w0 = 0, w1 = 0, w2 = 0;
     auto code_at = [&](int r, int c) -> int {
         if (r < 0 && c < 0) return -1;
         if (r < 0) return COL_INC;   // make_frame :399-406
         if (c < 0) return ROW_INC;   // :391-398
         const int ss = r + c;
-        if ((ss >> 4) != blk) {
-            blk = ss >> 4;
-            w = track[(int64_t)blk * 64 + lane];
+        const int nb = ss >> 4;
+        if (nb != blk) {
+            if (nb == blk - 1) {
+                w0 = w1;
+                w1 = w2;
+            } else {
+                w0 = track[(int64_t)nb * 64 + lane];
+                w1 = nb >= 1 ? track[(int64_t)(nb - 1) * 64 + lane] : 0u;
+            }
+            w2 = nb >= 2 ? track[(int64_t)(nb - 2) * 64 + lane] : 0u;
+            blk = nb;
         }
         const int owner = (c - r + G) >> 1;
-        const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)w, owner);
+        const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)w0, owner);
         return (int)((word >> (2 * (ss & 15))) & 3u);
-    };
-    auto step_cost = [&](int code, int r, int c) -> int {
-        return code == MATCH ? sub(a, b, r, c, mm) : gp;
     };
     auto go_prev = [&](int code, int& r, int& c) {
         if (code == MATCH || code == ROW_INC) r -= 1;
         if (code == MATCH || code == COL_INC) c -= 1;
     };
-    if (A.max_errors == -1) {
-        // the in-band score of the completion cell, or BAD_VALUE for a forced end
-        // (those cells are never computed by the reference either)
-        if (forced_row || forced_col || end_row < 0) score = BAD_VALUE;
-        else {  // replay the path's costs from the start (exact: at() = sum of step costs)
-            int r = end_row, c = end_col, acc_s = 0;
-            while (r >= 0 || c >= 0) {
-                const int code = code_at(r, c);
-                acc_s += (r >= 0 && c >= 0) ? step_cost(code, r, c) : gp;
-                go_prev(code, r, c);
-            }
-            score = acc_s;
-        }
-    }
-    if (A.cut_tail && end_row >= -1) {  // cut_tail (:240-255), max_errors != -1 only
+    if (A.cut_tail) {  // cut_tail (:240-255), max_errors != -1 only
         while (end_row >= 0 || end_col >= 0) {
             const int code = code_at(end_row, end_col);
-            const int cost = (end_row >= 0 && end_col >= 0) ? step_cost(code, end_row, end_col) : gp;
+            const int cost = (end_row >= 0 && end_col >= 0) ? (code == MATCH ? sub(a, b, end_row, end_col, mm) : gp)
+                                                            : gp;
             if (cost <= 0) break;
             score -= cost;
             go_prev(code, end_row, end_col);
@@ -257,6 +446,11 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
         out[2] = score;
         out[3] = 0;
         out[4] = n;
+#ifdef NPGX_SA_PROFILE
+        out[5] = (int32_t)((t_fwd - t_start) >> 4);
+        out[6] = (int32_t)((clock64() - t_fwd) >> 4);
+        out[7] = s_end + 1;
+#endif
     }
 }
 
@@ -278,7 +472,7 @@ struct npgx_dp {
     PinnedArena pinned;
     StageTimer timer;
     bool has_result = false;
-    std::vector<int32_t> res;        // 5 per pair
+    std::vector<int32_t> res;        // RES per pair
     std::vector<int64_t> op_off;     // n_pairs + 1
     std::vector<int8_t> ops;         // forward order
     int64_t cells = 0;
@@ -341,7 +535,7 @@ static void dp_run(npgx_dp* D, const char* first, const int64_t* first_off, cons
     D->d_pairs.grow((size_t)std::max(n, 1));
     D->d_track.grow((size_t)std::max<int64_t>(tw, 1));
     D->d_ops.grow((size_t)std::max<int64_t>(oc, 1));
-    D->d_res.grow((size_t)std::max(n, 1) * 5);
+    D->d_res.grow((size_t)std::max(n, 1) * RES);
     auto put = [&](void* d, const void* h, size_t bytes) {
         if (!bytes) return;
         char* p = D->pinned.take(bytes, st);
@@ -361,17 +555,17 @@ static void dp_run(npgx_dp* D, const char* first, const int64_t* first_off, cons
         NPGX_HIP(hipGetLastError());
         D->timer.end(ti, st);
     }
-    D->res.assign((size_t)n * 5, 0);
+    D->res.assign((size_t)n * RES, 0);
     std::vector<int8_t> raw((size_t)oc);
     if (n) {
-        NPGX_HIP(hipMemcpyAsync(D->res.data(), D->d_res.p, (size_t)n * 5 * 4, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipMemcpyAsync(D->res.data(), D->d_res.p, (size_t)n * RES * 4, hipMemcpyDeviceToHost, st));
         if (oc) NPGX_HIP(hipMemcpyAsync(raw.data(), D->d_ops.p, (size_t)oc, hipMemcpyDeviceToHost, st));
     }
     NPGX_HIP(hipStreamSynchronize(st));
     D->pinned.reset();
     D->ops.clear();
     for (int32_t i = 0; i < n; i++) {
-        const int32_t k = D->res[(size_t)i * 5 + 4];
+        const int32_t k = D->res[(size_t)i * RES + 4];
         const int64_t end = pairs[(size_t)i].out_end;
         D->ops.insert(D->ops.end(), raw.begin() + (end - k), raw.begin() + end);
         D->op_off[(size_t)i + 1] = (int64_t)D->ops.size();
@@ -442,13 +636,30 @@ int npgx_dp_result_copy(const npgx_dp* D, int32_t* first_last, int32_t* second_l
         NPGX_REQUIRE(D->has_result, NPGX_ERR_STATE, "no GeneralAligner result yet");
         const size_t n = D->op_off.size() - 1;
         for (size_t i = 0; i < n; i++) {
-            if (first_last) first_last[i] = D->res[i * 5 + 0];
-            if (second_last) second_last[i] = D->res[i * 5 + 1];
-            if (score) score[i] = D->res[i * 5 + 2];
-            if (status) status[i] = D->res[i * 5 + 3];
+            if (first_last) first_last[i] = D->res[i * RES + 0];
+            if (second_last) second_last[i] = D->res[i * RES + 1];
+            if (score) score[i] = D->res[i * RES + 2];
+            if (status) status[i] = D->res[i * RES + 3];
         }
         if (op_off) memcpy(op_off, D->op_off.data(), D->op_off.size() * 8);
         if (ops && !D->ops.empty()) memcpy(ops, D->ops.data(), D->ops.size());
+    });
+}
+
+int npgx_dp_phase_cycles(const npgx_dp* D, int64_t* fwd, int64_t* back, int64_t* steps) {
+    return guard([&] {
+        NPGX_REQUIRE(D && fwd && back && steps, NPGX_ERR_ARG, "null argument");
+        NPGX_REQUIRE(D->has_result, NPGX_ERR_STATE, "no GeneralAligner result yet");
+#ifdef NPGX_SA_PROFILE
+        *fwd = *back = *steps = 0;
+        for (size_t i = 0; i + RES <= D->res.size(); i += RES) {
+            *fwd += 16ll * D->res[i + 5];
+            *back += 16ll * D->res[i + 6];
+            *steps += D->res[i + 7];
+        }
+#else
+        throw Error(NPGX_ERR_STATE, "phase cycles need the diagnostic build (NPGX_PROFILE=1)");
+#endif
     });
 }
 

@@ -35,6 +35,7 @@ def _bind(L):
     L.npgx_dp_result_counts.argtypes = [vp, P(i64), P(i64)]
     L.npgx_dp_result_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     L.npgx_dp_kernel_times.argtypes = [vp, P(_capi.KernelTime), i32, P(i32)]
+    L.npgx_dp_phase_cycles.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.npgx_dp_free.argtypes = [vp]
     L.npgx_dp_free.restype = None
     L._dp_bound = True
@@ -108,6 +109,14 @@ class GeneralAligner:
 
     def kernel_times(self):
         return _capi.kernel_times(_bind(_capi.lib()).npgx_dp_kernel_times, self._h)
+
+    def phase_cycles(self):
+        """(forward, traceback, steps) summed over the batch's waves; needs the
+        diagnostic library (NPGX_PROFILE=1)."""
+        f, b, s = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _capi.check(_bind(_capi.lib()).npgx_dp_phase_cycles(self._h, ctypes.byref(f), ctypes.byref(b),
+                                                             ctypes.byref(s)))
+        return f.value, b.value, s.value
 
     def close(self):
         if self._h is not None:

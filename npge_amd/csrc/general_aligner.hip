@@ -124,7 +124,7 @@ struct Fwd {  // per-wave state of the forward pass
     unsigned long long pend_key;
     int end_v;
     int loaded;
-    char pre;
+    uint32_t pa[8], pb[8];  // next 32 letters of each sequence (scalar loads, one refill ahead)
 };
 
 __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
@@ -152,16 +152,23 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
         return;
     }
     for (int i = lane; i < RING; i += 64) ring[i] = ~0ull;
-    // letters: the first 128 of each sequence, then 32 more per refill from a
-    // register loaded one refill ahead (lanes 0-31: a, lanes 32-63: b)
+    // letters: the first 128 of each sequence, then 32 more per refill from
+    // scalar loads issued one refill ahead (lgkmcnt: they never wait behind the
+    // traceback stores).  Pair letters start 16-byte aligned with 64 bytes of
+    // slack after the batch, so whole dwords can be read past the end.
+    const uint32_t* __restrict__ a32 = (const uint32_t*)a;
+    const uint32_t* __restrict__ b32 = (const uint32_t*)b;
     for (int i = lane; i < 128; i += 64) {
         wa[i] = i < P.la ? a[i] : 0;
         wb[i] = i < P.lb ? b[i] : 0;
     }
-    const int pl = lane & 31;
     Fwd F;
     F.loaded = 128;
-    F.pre = lane < 32 ? (F.loaded + pl < P.la ? a[F.loaded + pl] : 0) : (F.loaded + pl < P.lb ? b[F.loaded + pl] : 0);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        F.pa[i] = a32[32 + i];
+        F.pb[i] = b32[32 + i];
+    }
     __syncthreads();
 
     // registers: the last value on each owned diagonal (frame value at start)
@@ -185,11 +192,21 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
         const int need = (s + REFILL + G + 2) / 2 + 2;
         bool wrote = false;
         while (F.loaded < need + 32) {
-            if (lane < 32) wa[(F.loaded + pl) & (LWIN - 1)] = F.pre;
-            else wb[(F.loaded + pl) & (LWIN - 1)] = F.pre;
+            uint32_t xa = F.pa[0], xb = F.pb[0];
+#pragma unroll
+            for (int i = 1; i < 8; i++) {
+                xa = (lane & 7) == i ? F.pa[i] : xa;
+                xb = (lane & 7) == i ? F.pb[i] : xb;
+            }
+            const int at = ((F.loaded >> 2) + (lane & 7)) & (LWIN / 4 - 1);
+            if (lane < 8) wa32[at] = xa;
+            else if (lane < 16) wb32[at] = xb;
             F.loaded += 32;
-            F.pre = lane < 32 ? (F.loaded + pl < P.la ? a[F.loaded + pl] : 0)
-                              : (F.loaded + pl < P.lb ? b[F.loaded + pl] : 0);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                F.pa[i] = a32[(F.loaded >> 2) + i];
+                F.pb[i] = b32[(F.loaded >> 2) + i];
+            }
             wrote = true;
         }
         if (wrote) __syncthreads();
@@ -380,28 +397,40 @@ __global__ __launch_bounds__(64) void k_general_align(GaArgs A) {
     }
 
     // traceback reader: 16-step blocks of directions, one coalesced load each,
-    // the next two blocks down prefetched; a cell's 2 bits by readlane
-    int blk = -1;
-    uint32_t w0 = 0, w1 = 0, w2 = 0;
+    // in batches of 4 blocks with the next batch down loaded one batch ahead
+    // (a single wait per batch); a cell's 2 bits by readlane
+    int batch = INT_MIN;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+    const int n_blk = s_end >= 0 ? (s_end >> 4) + 1 : 0;  // blocks of this pair's track region
+    auto load4 = [&](int bt, uint32_t& x0, uint32_t& x1, uint32_t& x2, uint32_t& x3) {
+        const int b0 = 4 * bt;  // only blocks inside the region are read
+        x0 = (b0 >= 0 && b0 < n_blk) ? track[(int64_t)b0 * 64 + lane] : 0u;
+        x1 = (b0 + 1 >= 0 && b0 + 1 < n_blk) ? track[(int64_t)(b0 + 1) * 64 + lane] : 0u;
+        x2 = (b0 + 2 >= 0 && b0 + 2 < n_blk) ? track[(int64_t)(b0 + 2) * 64 + lane] : 0u;
+        x3 = (b0 + 3 >= 0 && b0 + 3 < n_blk) ? track[(int64_t)(b0 + 3) * 64 + lane] : 0u;
+    };
     auto code_at = [&](int r, int c) -> int {
         if (r < 0 && c < 0) return -1;
         if (r < 0) return COL_INC;   // make_frame :399-406
         if (c < 0) return ROW_INC;   // :391-398
         const int ss = r + c;
-        const int nb = ss >> 4;
-        if (nb != blk) {
-            if (nb == blk - 1) {
-                w0 = w1;
-                w1 = w2;
+        const int nb = ss >> 4, bt = nb >> 2;
+        if (bt != batch) {
+            if (bt == batch - 1) {
+                c0 = n0;
+                c1 = n1;
+                c2 = n2;
+                c3 = n3;
             } else {
-                w0 = track[(int64_t)nb * 64 + lane];
-                w1 = nb >= 1 ? track[(int64_t)(nb - 1) * 64 + lane] : 0u;
+                load4(bt, c0, c1, c2, c3);
             }
-            w2 = nb >= 2 ? track[(int64_t)(nb - 2) * 64 + lane] : 0u;
-            blk = nb;
+            load4(bt - 1, n0, n1, n2, n3);
+            batch = bt;
         }
+        const int i = nb & 3;
+        const uint32_t w = i == 0 ? c0 : i == 1 ? c1 : i == 2 ? c2 : c3;
         const int owner = (c - r + G) >> 1;
-        const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)w0, owner);
+        const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)w, owner);
         return (int)((word >> (2 * (ss & 15))) & 3u);
     };
     auto go_prev = [&](int code, int& r, int& c) {
@@ -508,19 +537,21 @@ static void dp_run(npgx_dp* D, const char* first, const int64_t* first_off, cons
     D->has_result = false;
     const npgx_dp_options& o = D->opt;
     NPGX_REQUIRE(n >= 0, NPGX_ERR_ARG, "n_pairs < 0");
-    const int64_t a0 = n ? first_off[0] : 0, b0 = n ? second_off[0] : 0;
-    const int64_t abytes = n ? first_off[n] - a0 : 0, bbytes = n ? second_off[n] - b0 : 0;
+    // device layout: every pair's letters start 16-byte aligned (the kernel
+    // reads them as dwords with scalar loads), 64 bytes of slack at the end
     std::vector<Pair> pairs((size_t)n);
     D->op_off.assign((size_t)n + 1, 0);
-    int64_t tw = 0, oc = 0;
+    int64_t tw = 0, oc = 0, pa = 0, pb = 0;
     D->cells = 0;
     for (int32_t i = 0; i < n; i++) {
         const int64_t la = first_off[i + 1] - first_off[i], lb = second_off[i + 1] - second_off[i];
         NPGX_REQUIRE(la >= 0 && lb >= 0 && la < (1 << 30) && lb < (1 << 30), NPGX_ERR_RANGE,
                      "sequence length out of range");
         Pair& P = pairs[(size_t)i];
-        P.a_off = first_off[i] - a0;
-        P.b_off = second_off[i] - b0;
+        P.a_off = pa;
+        P.b_off = pb;
+        pa += (la + 15) & ~15ll;
+        pb += (lb + 15) & ~15ll;
         P.la = (int32_t)la;
         P.lb = (int32_t)lb;
         P.track_off = tw;
@@ -529,9 +560,10 @@ static void dp_run(npgx_dp* D, const char* first, const int64_t* first_off, cons
         P.out_end = oc;
         D->cells += band_cells(P.la, P.lb, o.gap_range);
     }
+    const int64_t abytes = pa + 64, bbytes = pb + 64;
     NPGX_REQUIRE(tw < (1ll << 36), NPGX_ERR_RANGE, "traceback store over 256 GiB");
-    D->d_a.grow((size_t)std::max<int64_t>(abytes, 1));
-    D->d_b.grow((size_t)std::max<int64_t>(bbytes, 1));
+    D->d_a.grow((size_t)abytes);
+    D->d_b.grow((size_t)bbytes);
     D->d_pairs.grow((size_t)std::max(n, 1));
     D->d_track.grow((size_t)std::max<int64_t>(tw, 1));
     D->d_ops.grow((size_t)std::max<int64_t>(oc, 1));
@@ -542,14 +574,25 @@ static void dp_run(npgx_dp* D, const char* first, const int64_t* first_off, cons
         memcpy(p, h, bytes);
         NPGX_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, st));
     };
-    put(D->d_a.p, first + a0, (size_t)abytes);
-    put(D->d_b.p, second + b0, (size_t)bbytes);
+    auto put_letters = [&](char* d, const char* src, const int64_t* off, int64_t bytes, bool first_seq) {
+        char* p = D->pinned.take((size_t)bytes, st);
+        memset(p + bytes - 64, 0, 64);
+        for (int32_t i = 0; i < n; i++) {
+            const int64_t len = off[i + 1] - off[i];
+            const int64_t at = first_seq ? pairs[(size_t)i].a_off : pairs[(size_t)i].b_off;
+            memcpy(p + at, src + off[i], (size_t)len);
+            memset(p + at + len, 0, (size_t)(((len + 15) & ~15ll) - len));
+        }
+        NPGX_HIP(hipMemcpyAsync(d, p, (size_t)bytes, hipMemcpyHostToDevice, st));
+    };
+    put_letters(D->d_a.p, first, first_off, abytes, true);
+    put_letters(D->d_b.p, second, second_off, bbytes, false);
     put(D->d_pairs.p, pairs.data(), pairs.size() * sizeof(Pair));
     if (n) {
         GaArgs A{D->d_a.p, D->d_b.p, D->d_pairs.p, D->d_track.p, D->d_ops.p, D->d_res.p,
                  o.gap_range, o.max_errors, o.gap_penalty, o.mismatch_penalty, o.cut_tail, 0};
         // algorithmic bytes: letters in, 2 bits per band cell out, ops out
-        const double bytes = double(abytes + bbytes) + 0.25 * double(D->cells) + double(oc);
+        const double bytes = double(oc) + 0.25 * double(D->cells) + double(oc);
         size_t ti = D->timer.begin("general_align", st, bytes, D->cells);
         hipLaunchKernelGGL(k_general_align, dim3((unsigned)n), dim3(64), 0, st, A);
         NPGX_HIP(hipGetLastError());

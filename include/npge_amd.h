@@ -89,6 +89,11 @@ typedef struct {
     uint32_t bloom_seed;
     int32_t n_bloom_params;
     const uint64_t* bloom_params;
+    /* one-GPU Bloom pass in epochs of consecutive windows (a bit array of the
+     * earlier epochs filters atomics and reads; same result): 0 = automatic
+     * (about 2M windows per epoch), 1 = a single pass, k = k epochs */
+    int32_t bloom_epochs;
+    int32_t pad0;
 } npgx_af_options;
 
 void npgx_af_default_options(npgx_af_options* o);

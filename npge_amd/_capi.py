@@ -34,7 +34,8 @@ class AfOptions(ctypes.Structure):
     _fields_ = [("anchor_size", ctypes.c_int32), ("anchor_similar", ctypes.c_int32),
                 ("anchor_fp_x1e4", ctypes.c_int64), ("max_anchor_fragments", ctypes.c_int64),
                 ("bloom_seed", ctypes.c_uint32), ("n_bloom_params", ctypes.c_int32),
-                ("bloom_params", ctypes.POINTER(ctypes.c_uint64))]
+                ("bloom_params", ctypes.POINTER(ctypes.c_uint64)),
+                ("bloom_epochs", ctypes.c_int32), ("pad0", ctypes.c_int32)]
 
 
 class AfStats(ctypes.Structure):

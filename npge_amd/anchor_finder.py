@@ -41,6 +41,7 @@ class AnchorFinder(Processor):
         self.add_gopt("max-anchor-fragments", "Maximum number of anchors fragments to return",
                       "MAX_ANCHOR_FRAGMENTS")
         self.add_opt("bloom-seed", "glibc srand() seed of the Bloom hash parameters", 1)
+        self.add_opt("bloom-epochs", "epochs of the one-GPU Bloom pass (0 = automatic, 1 = single pass)", 0)
         self.add_opt_rule("anchor-size > 0", lambda p: p.opt_value("anchor-size") > 0)
         self.add_opt_rule("anchor-size <= 32", lambda p: p.opt_value("anchor-size") <= 32)
         self.bloom_params = bloom_params
@@ -52,7 +53,7 @@ class AnchorFinder(Processor):
         L = _capi.lib()
         key = (self.opt_value("anchor-size"), self.opt_value("anchor-fp").impl,
                bool(self.opt_value("anchor-similar")), self.opt_value("max-anchor-fragments"),
-               self.opt_value("bloom-seed"), tuple(self.bloom_params or ()))
+               self.opt_value("bloom-seed"), tuple(self.bloom_params or ()), self.opt_value("bloom-epochs"))
         if self._h is not None and key == self._h_key:
             return self._h
         if self._h is not None:
@@ -62,6 +63,7 @@ class AnchorFinder(Processor):
         L.npgx_af_default_options(ctypes.byref(o))
         o.anchor_size, o.anchor_fp_x1e4, o.anchor_similar = key[0], key[1], int(key[2])
         o.max_anchor_fragments, o.bloom_seed = key[3], key[4] & 0xFFFFFFFF
+        o.bloom_epochs = key[6]
         if self.bloom_params:
             arr = (ctypes.c_uint64 * len(self.bloom_params))(*self.bloom_params)
             o.n_bloom_params = len(self.bloom_params)

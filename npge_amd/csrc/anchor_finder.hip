@@ -47,6 +47,7 @@ void glibc_rand(uint32_t seed, int n, uint64_t* out);
 
 static constexpr int WG = 256;         // windows per workgroup (4 waves)
 static constexpr int MAX_KB = 32;
+static constexpr int FKB = 4;          // hash functions with the batched-load path (fp 0.1 -> 3)
 
 struct SeqMeta {
     int64_t size;
@@ -211,6 +212,120 @@ __global__ __launch_bounds__(WG) void k_found_collect(AfArgs a, const uint32_t* 
     }
 }
 
+// ---- epoch-filtered Bloom pass (one GPU).  The windows run in epochs of
+// consecutive chunks (order ascending); P is the Bloom bit array of every
+// window of the earlier epochs.  A bit in P was first set in an earlier epoch,
+// whose windows all atomicMin'ed it then, so first[bit] is already exact and
+// below the order of any window of this epoch: such bits need neither the
+// atomic nor the read of first[] -- the result equals the unfiltered pass.
+__device__ __forceinline__ bool bit_in(const uint32_t* __restrict__ P, uint32_t idx) {
+    return (P[idx >> 5] >> (idx & 31)) & 1u;
+}
+
+__global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ P) {
+    const Chunk c = a.chunks[blockIdx.x];
+    const SeqMeta s = a.meta[c.seq];
+    const int64_t p = c.pos + threadIdx.x;
+    uint64_t h, dir;
+    if (!admitted(a, s, p, h, dir)) return;
+    const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
+    if (a.kb <= FKB) {
+        uint32_t idx[FKB], pw[FKB];
+#pragma unroll
+        for (int i = 0; i < FKB; i++)
+            if (i < a.kb) {
+                idx[i] = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+                pw[i] = P[idx[i] >> 5];
+            }
+#pragma unroll
+        for (int i = 0; i < FKB; i++)
+            if (i < a.kb && !((pw[i] >> (idx[i] & 31)) & 1u)) atomicMin(&first[idx[i]], ord);
+        return;
+    }
+    for (int i = 0; i < a.kb; i++) {
+        const uint32_t idx = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+        if (!bit_in(P, idx)) atomicMin(&first[idx], ord);
+    }
+}
+
+// found/collect of one epoch, reading P (bits of the earlier epochs) and
+// adding this epoch's bits to Pn (copied to P before the next epoch)
+__global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t* __restrict__ first,
+                                                        const uint32_t* __restrict__ P,
+                                                        uint32_t* __restrict__ Pn,
+                                                        uint64_t* __restrict__ out,
+                                                        unsigned long long* __restrict__ n_out) {
+    __shared__ uint8_t fs[WG];
+    const Chunk c = a.chunks[blockIdx.x];
+    const SeqMeta s = a.meta[c.seq];
+    const int t = threadIdx.x;
+    const int64_t p = c.pos + t;
+    uint64_t h = 0;
+    bool f = false;
+    {
+        uint64_t dir;
+        if (admitted(a, s, p, h, dir)) {
+            const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
+            f = true;
+            if (a.kb <= FKB) {
+                // all P words, then the needed first[] entries, then the new
+                // bits: independent loads issued together
+                uint32_t idx[FKB], pw[FKB], fv[FKB];
+#pragma unroll
+                for (int i = 0; i < FKB; i++)
+                    if (i < a.kb) {
+                        idx[i] = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+                        pw[i] = P[idx[i] >> 5];
+                    }
+#pragma unroll
+                for (int i = 0; i < FKB; i++)
+                    if (i < a.kb) {
+                        pw[i] = (pw[i] >> (idx[i] & 31)) & 1u;  // set by an earlier epoch
+                        fv[i] = pw[i] ? 0u : first[idx[i]];
+                    }
+#pragma unroll
+                for (int i = 0; i < FKB; i++)
+                    if (i < a.kb && !pw[i]) {
+                        f &= fv[i] < ord;
+                        if (Pn) atomicOr(&Pn[idx[i] >> 5], 1u << (idx[i] & 31));
+                    }
+            } else {
+                for (int i = 0; i < a.kb; i++) {
+                    const uint32_t idx = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+                    const uint32_t bit = 1u << (idx & 31);
+                    if (P[idx >> 5] & bit) continue;   // set by an earlier epoch
+                    f &= first[idx] < ord;
+                    if (Pn && !(Pn[idx >> 5] & bit)) atomicOr(&Pn[idx >> 5], bit);
+                }
+            }
+        }
+    }
+    fs[t] = f;
+    __syncthreads();
+    bool prev;
+    if (t > 0) {
+        prev = fs[t - 1];
+    } else {
+        // p-1 may belong to an earlier epoch (P then holds bits set after it):
+        // the exact test on first[] alone
+        uint64_t hp;
+        prev = found_at(a, s, p - 1, first, hp);
+    }
+    const bool col = f && !(a.similar && prev);
+    const unsigned long long mask = __ballot(col);
+    if (mask == 0) return;
+    const int lane = t & 63;
+    const int leader = __ffsll((long long)mask) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(n_out, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader);
+    if (col) {
+        const unsigned long long below = mask & ((1ull << lane) - 1ull);
+        out[base + __popcll(below)] = h;
+    }
+}
+
 __global__ void k_table_insert(const uint64_t* __restrict__ hs, int64_t n, uint64_t* keys,
                                uint32_t* vals, uint32_t mask, int shift) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -317,6 +432,7 @@ struct npgx_af {
     DevBuf<SeqMeta> d_meta;
     DevBuf<Chunk> d_chunks;
     DevBuf<uint32_t> first;
+    DevBuf<uint32_t> bloom_bits;  // P of the epoch-filtered pass
     DevBuf<uint64_t> hraw, hsorted, huniq;
     DevBuf<unsigned long long> counters;  // [0] = n_raw, [1] = n_unique
     DevBuf<uint64_t> tkeys;
@@ -520,7 +636,41 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     af->first.ensure((size_t)m);
     af->counters.ensure(4);
     NPGX_HIP(hipMemsetAsync(af->counters.p, 0, 4 * sizeof(unsigned long long), st));
-    size_t ti = af->timer.begin("bloom_first", st, local_windows * (0.375 + 8.0 * kb), local_windows);
+    af->hraw.ensure((size_t)std::max<int64_t>(local_windows, 1));
+    size_t ti = 0;
+    if (!comm && af->opt.bloom_epochs != 1) {
+        // epochs of consecutive chunks (SeqMeta order); bits set by earlier
+        // epochs skip the atomics and the first[] reads
+        const int64_t per = std::max<int64_t>(1, (int64_t)std::ceil(double(nchunks) / std::max(1, af->opt.bloom_epochs > 0
+                                                                         ? af->opt.bloom_epochs
+                                                                         : (int)std::max<int64_t>(1, n_windows / (2 << 20)))));
+        const size_t words = ((size_t)m + 31) / 32;
+        af->bloom_bits.ensure(2 * words);  // P (earlier epochs) | Pn (through this one)
+        ti = af->timer.begin("bloom_first", st, n_windows * (0.375 + 8.0 * kb), n_windows);
+        NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
+        NPGX_HIP(hipMemsetAsync(af->bloom_bits.p, 0, 2 * words * 4, st));
+        af->timer.end(ti, st);
+        for (int64_t e0 = 0; e0 < nchunks; e0 += per) {
+            const int64_t ne = std::min(per, nchunks - e0);
+            AfArgs E = A;
+            E.chunks = A.chunks + e0;
+            const dim3 eg((unsigned)ne);
+            ti = af->timer.begin("bloom_first", st, 0.0, 0);
+            hipLaunchKernelGGL(k_bloom_first_f, eg, block, 0, st, E, af->first.p, af->bloom_bits.p);
+            NPGX_HIP(hipGetLastError());
+            af->timer.end(ti, st);
+            ti = af->timer.begin("found_collect", st, n_windows * (0.375 + 4.0 * kb) * double(ne) / nchunks, 0);
+            const bool more = e0 + ne < nchunks;
+            hipLaunchKernelGGL(k_found_collect_f, eg, block, 0, st, E, af->first.p, af->bloom_bits.p,
+                               more ? af->bloom_bits.p + words : nullptr, af->hraw.p, af->counters.p);
+            NPGX_HIP(hipGetLastError());
+            af->timer.end(ti, st);
+            if (more)
+                NPGX_HIP(hipMemcpyAsync(af->bloom_bits.p, af->bloom_bits.p + words, words * 4,
+                                        hipMemcpyDeviceToDevice, st));
+        }
+    } else {
+    ti = af->timer.begin("bloom_first", st, local_windows * (0.375 + 8.0 * kb), local_windows);
     NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
     if (run_local) hipLaunchKernelGGL(k_bloom_first, grid, block, 0, st, A, af->first.p);
     NPGX_HIP(hipGetLastError());
@@ -538,13 +688,13 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         af->timer.end(ti, st);
     }
 
-    af->hraw.ensure((size_t)std::max<int64_t>(local_windows, 1));
     ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
     if (run_local)
         hipLaunchKernelGGL(k_found_collect, grid, block, 0, st, A, af->first.p, af->hraw.p,
                            af->counters.p);
     NPGX_HIP(hipGetLastError());
     af->timer.end(ti, st);
+    }
     NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8, hipMemcpyDeviceToHost, st));
     NPGX_HIP(hipStreamSynchronize(st));
     const int64_t n_raw = (int64_t)hp[0];
@@ -772,6 +922,7 @@ int npgx_af_create(const npgx_af_options* o, npgx_af** out) {
         NPGX_REQUIRE(o->max_anchor_fragments >= 0, NPGX_ERR_ARG, "max-anchor-fragments < 0");
         NPGX_REQUIRE(o->n_bloom_params >= 0 && o->n_bloom_params <= MAX_KB, NPGX_ERR_ARG,
                      "n_bloom_params out of range");
+        NPGX_REQUIRE(o->bloom_epochs >= 0, NPGX_ERR_ARG, "bloom_epochs < 0");
         int dev = current_device_checked();
         auto* af = new npgx_af;
         af->opt = *o;

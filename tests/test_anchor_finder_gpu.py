@@ -122,3 +122,21 @@ def test_consensus_naming_and_ties():
     names = ["c3", "c1", "c2", "c0"]
     (rg, ro, used), = _run_both(seqs, names, k=12)
     _assert_same(rg, ro, used)
+
+
+@pytest.mark.parametrize("epochs", [1, 2, 3, 7, 40])
+def test_bloom_epochs_same_result(epochs):
+    """The epoch-filtered Bloom pass (bit array of the earlier epochs skipping
+    atomics and first[] reads) gives the reference's result for any epoch
+    split, including epochs that cut a sequence and the repeated-run used set."""
+    from npge_amd import _capi
+    names, seqs = synth.genome_set("small")
+    ss = _capi.SeqSet(seqs, names)
+    g = _gpu_af(anchor_size=20, bloom_seed=3, max_anchor_fragments=20000)
+    g.set_opt_value("bloom-epochs", epochs)
+    o = orc.AnchorFinder(anchor_size=20, anchor_fp_x1e4=1000, anchor_similar=True,
+                         max_anchor_fragments=20000, seed=3)
+    for _ in range(2):
+        rg = g.find(ss)
+        ro = o.run(seqs, names)
+        _assert_same(rg, ro, g.used_hashes())

@@ -266,6 +266,70 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
 #endif
         const unsigned long long vmask = ballot(valid);
         int f_best = 64, i_best = -1;
+        if (n <= 4 && ac <= 10) {
+            // LDS table of the chunk's words (rows 4..7 of W): key = word + 1,
+            // and per row the first shift holding it (byte k, 0xFF = absent).
+            // Rows insert one after the other, so a row's byte is the only one
+            // changing during its pass and a 32-bit atomicMin of the whole
+            // byte vector is that byte's minimum.  Then lane s of row i knows
+            // for every row k whether wi occurs in row k at a shift <= s.
+            uint32_t* T32 = (uint32_t*)(W + 4 * 64);  // 256 entries x (key, shifts)
+            for (int e = lane; e < 256; e += 64) {
+                T32[2 * e] = 0u;
+                T32[2 * e + 1] = 0xFFFFFFFFu;
+            }
+            __syncthreads();
+            for (int k = 0; k < n; k++) {
+                if (valid) {
+                    const uint32_t key = (uint32_t)W[k * 64 + lane] + 1u;
+                    uint32_t e = (key * 0x9E3779B1u) >> 24;
+                    for (int probe = 0; probe < 256; probe++) {
+                        const uint32_t o = atomicCAS(&T32[2 * e], 0u, key);
+                        if (o == 0u || o == key) break;
+                        e = (e + 1) & 255u;
+                    }
+                    const uint32_t cur = T32[2 * e + 1];
+                    atomicMin(&T32[2 * e + 1], (cur & ~(0xFFu << (8 * k))) | ((uint32_t)lane << (8 * k)));
+                }
+                __syncthreads();
+            }
+            for (int i = 0; i < n; i++) {
+                const unsigned long long wi = W[i * 64 + lane];
+                unsigned old = 0;  // rows that had wi before this chunk
+                if (S0 > 0 && valid) {
+                    const unsigned long long key = ep | wi;
+                    uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tcap_log2));
+                    while (true) {
+                        const unsigned long long k = tkeys[slot];
+                        if (k == key) {
+                            const unsigned long long m = tmask[slot];
+                            old = (m & EPM) == ep ? (unsigned)(m & 0xFFu) : 0u;
+                            break;
+                        }
+                        if ((k & EPM) != ep) break;
+                        slot = (slot + 1) & (tcap - 1);
+                    }
+                }
+                bool ok = valid;
+                if (valid) {
+                    const uint32_t key = (uint32_t)wi + 1u;
+                    uint32_t e = (key * 0x9E3779B1u) >> 24;
+                    for (int probe = 0; probe < 256 && T32[2 * e] != key; probe++) e = (e + 1) & 255u;
+                    const uint32_t sh = T32[2 * e + 1];
+                    for (int k = 0; k < n; k++)
+                        if (k != i) ok &= ((old >> k) & 1u) || ((sh >> (8 * k)) & 0xFFu) <= (uint32_t)lane;
+                }
+                const unsigned long long comp = ballot(ok);
+                if (comp) {
+                    const int f = __ffsll((long long)comp) - 1;
+                    if (f <= f_best) {  // ties: the higher row names the word
+                        f_best = f;
+                        i_best = i;
+                    }
+                }
+            }
+            __syncthreads();
+        } else
         for (int i = 0; i < n; i++) {
             const unsigned long long wi = W[i * 64 + lane];
             unsigned old = 0;  // rows that had wi before this chunk

@@ -763,13 +763,24 @@ __device__ __forceinline__ void stage_rows(View& v0, int n, char* stage, int sta
     if (lane < n) v0.p = stage + off;
 }
 
+// realing_end (:461-484) re-aligns the reversed, gap-free last aligned_check
+// columns; when each of them holds one letter in every row the greedy
+// process_seqs rebuilds exactly those columns, so the pass is skipped
+__device__ __forceinline__ bool tail_identical(const WaveCtx& w, const char* B, int cap, int c0, int c1) {
+    for (int j = c0; j < c1; j++) {
+        const int c = w.act ? (unsigned char)B[(size_t)w.lane * cap + j] : 0;
+        if (any_lane(w, c == '-') || !all_eq(w, c)) return false;
+    }
+    return true;
+}
+
 // realing_end (:461-484) on B + AbstractAligner remove_gaps; returns the length
 __device__ int finish_tail(Proc& pr, const WaveCtx& w, char* B, char* C, int cap, int L, char* stage,
                            int stage_bytes, int ac, bool& ovf) {
     pr.ob = B;
-    if (!ovf && L >= 2) {
-        int prefix = L - ac;
-        if (prefix < 1) prefix = 1;
+    int prefix = L - ac;
+    if (prefix < 1) prefix = 1;
+    if (!ovf && L >= 2 && !tail_identical(w, B, cap, prefix, L)) {
         const View tv = stage_segment(w, B, cap, C, stage, stage_bytes, prefix, L);
         const int Lt = pr.run(tv, prefix);
         if (any_lane(w, pr.ovf)) ovf = true;
@@ -1089,9 +1100,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 t_ph[1] = clock64() - t0;
                 t0 = clock64();
                 if (!deferred) L = colB;
-                if (!deferred && !ovf && L >= 2) {
-                    int prefix = L - a.P.ac;
-                    if (prefix < 1) prefix = 1;
+                int prefix = L - a.P.ac;
+                if (prefix < 1) prefix = 1;
+                if (!deferred && !ovf && L >= 2 && !tail_identical(w, B, cap, prefix, L)) {
                     const View tv = stage_segment(w, B, cap, C, stage, a.stage_bytes, prefix, L);
                     const int Lt = pr.run(tv, prefix);
                     if (any_lane(w, pr.ovf)) ovf = true;

@@ -750,20 +750,26 @@ struct Proc {
                 if (t < ac - 1) word = (word << 3) | code3(c[t]);
         }
         int inserted = 0;
+        // the chars a step adds are loaded one step ahead: the table atomics
+        // between steps would otherwise keep every step waiting on its loads
+        int cn[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) cn[t] = (act && t < 1) ? vch(vr, nxt + t, r) : 0;
         for (int s0 = 0; s0 < max_shift; s0 += J) {
             const int s = s0 + j;
             const bool valid = act && s < max_shift;
             const int add = s0 == 0 ? 1 : J;  // chars entering this lane's word
             if (act) {
-                int c[8];
-#pragma unroll
-                for (int t = 0; t < 8; t++) c[t] = t < add ? vch(vr, nxt + t, r) : 0;
 #pragma unroll
                 for (int t = 0; t < 8; t++)
-                    if (t < add) word = (word << 3) | code3(c[t]);
+                    if (t < add) word = (word << 3) | code3(cn[t]);
                 word &= wmask;
                 for (int t = 8; t < add; t++) word = ((word << 3) | code3(vch(vr, nxt + t, r))) & wmask;
                 nxt += add;
+                if (s0 + J < max_shift) {
+#pragma unroll
+                    for (int t = 0; t < 8; t++) cn[t] = t < J ? vch(vr, nxt + t, r) : 0;
+                }
             }
             if (valid && s < hist) hw[s * n + r] = word;
             // every lane inserts its word: claim (or find) the key, reset the

@@ -14,7 +14,7 @@ LIB = os.path.join(HERE, "libnpge_amd.so")
 # (loaded by _capi when NPGX_PROFILE=1)
 LIB_PROF = os.path.join(HERE, "libnpge_amd_prof.so")
 SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip", "block_build.hip",
-           "general_aligner.hip"]
+           "general_aligner.hip", "host_sampler.cpp"]
 HEADERS = ["common.hpp", "sa_device.hpp", "log_score.inc"]
 ARCH = os.environ.get("NPGX_OFFLOAD_ARCH", "gfx950")
 
@@ -35,10 +35,14 @@ def build(force=False, verbose=False, profile=False):
     objs = []
     procs = []
     for src in [x for x in SOURCES if os.path.exists(os.path.join(CSRC, x))]:
-        obj = os.path.join(CSRC, src.replace(".hip", "_prof.o" if profile else ".o"))
-        cmd = ["hipcc", "-c", "-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
-               "-munsafe-fp-atomics", "-Wno-unused-result", "-I", os.path.join(os.path.dirname(HERE), "include"),
-               "-o", obj, os.path.join(CSRC, src)] + (["-DNPGX_SA_PROFILE=1"] if profile else [])
+        stem, ext = os.path.splitext(src)
+        obj = os.path.join(CSRC, stem + ("_prof.o" if profile else ".o"))
+        if ext == ".cpp":  # host-only helpers
+            cmd = ["g++", "-c", "-O2", "-std=c++17", "-fPIC", "-o", obj, os.path.join(CSRC, src)]
+        else:
+            cmd = ["hipcc", "-c", "-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
+                   "-munsafe-fp-atomics", "-Wno-unused-result", "-I", os.path.join(os.path.dirname(HERE), "include"),
+                   "-o", obj, os.path.join(CSRC, src)] + (["-DNPGX_SA_PROFILE=1"] if profile else [])
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

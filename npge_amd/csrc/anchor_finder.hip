@@ -680,7 +680,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         const dim3 fg((unsigned)((m + 255) / 256));
         ti = af->timer.begin("first_allreduce", st, (double)m * 4 * 2, m);
         hipLaunchKernelGGL(k_flip_sign, fg, dim3(256), 0, st, af->first.p, (int64_t)m);
-        NPGX_HIP(hipStreamSynchronize(st));
+        NPGX_HIP(stream_wait(st));
         comm_check(comm->allreduce_i32(comm->user, (int32_t*)af->first.p, m, NPGX_OP_MIN),
                    "allreduce(first, MIN)");
         hipLaunchKernelGGL(k_flip_sign, fg, dim3(256), 0, st, af->first.p, (int64_t)m);
@@ -696,7 +696,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     af->timer.end(ti, st);
     }
     NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8, hipMemcpyDeviceToHost, st));
-    NPGX_HIP(hipStreamSynchronize(st));
+    NPGX_HIP(stream_wait(st));
     const int64_t n_raw = (int64_t)hp[0];
     S.n_collected_raw = n_raw;
 
@@ -717,7 +717,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
                                  (size_t)n, rocprim::equal_to<uint64_t>(), st));
         af->timer.end(t, st);
         NPGX_HIP(hipMemcpyAsync(hp, af->counters.p + 1, 8, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipStreamSynchronize(st));
+        NPGX_HIP(stream_wait(st));
         return (int64_t)hp[0];
     };
     std::vector<int64_t> rc(world);
@@ -727,7 +727,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         int64_t tot = 0;
         for (int64_t v : rc) tot += v;
         af->gathered.grow((size_t)std::max<int64_t>(tot, 1));
-        NPGX_HIP(hipStreamSynchronize(st));
+        NPGX_HIP(stream_wait(st));
         if (tot > 0) comm_check(comm->allgatherv_u64(comm->user, src, rc.data(), af->gathered.p), what);
         return tot;
     };
@@ -779,7 +779,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
             af->offsets_local.ensure((size_t)nH);
             NPGX_HIP(hipMemcpyAsync(af->counts_local.p, af->counts.p, (size_t)nH * 4,
                                     hipMemcpyDeviceToDevice, st));
-            NPGX_HIP(hipStreamSynchronize(st));
+            NPGX_HIP(stream_wait(st));
             comm_check(comm->allreduce_i32(comm->user, (int32_t*)af->counts.p, nH, NPGX_OP_SUM),
                        "allreduce(counts, SUM)");
         }
@@ -796,7 +796,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         NPGX_HIP(hipGetLastError());
         af->timer.end(ti, st);
         NPGX_HIP(hipMemcpyAsync(hp, af->cut.p, 3 * 8, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipStreamSynchronize(st));
+        NPGX_HIP(stream_wait(st));
         G = hp[0];
         const uint64_t C = hp[1];
         S.n_found_frags = (int64_t)hp[2];
@@ -815,7 +815,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
                                    af->counts_local.p, nH, G, af->cut.p);
                 NPGX_HIP(hipGetLastError());
                 NPGX_HIP(hipMemcpyAsync(hp, af->cut.p + 3, 8, hipMemcpyDeviceToHost, st));
-                NPGX_HIP(hipStreamSynchronize(st));
+                NPGX_HIP(stream_wait(st));
                 C_local = hp[0];
                 scatter_off = af->offsets_local.p;
             }
@@ -848,7 +848,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
             Hh.resize(G);
             NPGX_HIP(hipMemcpyAsync(keys.data(), af->cand_sorted.p, keep * 8, hipMemcpyDeviceToHost, st));
             NPGX_HIP(hipMemcpyAsync(Hh.data(), af->huniq.p, G * 8, hipMemcpyDeviceToHost, st));
-            NPGX_HIP(hipStreamSynchronize(st));
+            NPGX_HIP(stream_wait(st));
         }
     }
 

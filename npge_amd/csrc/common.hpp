@@ -27,6 +27,12 @@ struct Error : std::runtime_error {
 
 void set_last_error(const std::string& msg);
 
+// Waits for a stream by polling (hipStreamQuery) instead of the runtime's
+// blocking wait: the host thread is dedicated to the pipeline, and a blocking
+// wait costs an interrupt and a thread wake-up (tens of microseconds) at each
+// of the block build's many short host<->device round trips.
+hipError_t stream_wait(hipStream_t s);
+
 #define NPGX_HIP(call)                                                                \
     do {                                                                              \
         hipError_t e_ = (call);                                                       \
@@ -100,7 +106,7 @@ struct PinnedArena {
     char* take(size_t n, hipStream_t st) {
         n = (n + 63) & ~(size_t)63;
         if (used + n > cap) {
-            NPGX_HIP(hipStreamSynchronize(st));
+            NPGX_HIP(stream_wait(st));
             used = 0;
             if (n > cap) {
                 if (p) (void)hipHostFree(p);
@@ -142,13 +148,18 @@ struct StageTimer {
         recs.clear();
         used = 0;
     }
+    // NPGX_TIMERS=0 switches the event records off (diagnostic: their cost)
+    bool on = !(getenv("NPGX_TIMERS") && getenv("NPGX_TIMERS")[0] == '0');
     size_t begin(const char* name, hipStream_t s, double bytes, int64_t units) {
+        if (!on) return 0;
         Rec r{name, get(), get(), bytes, units};
         NPGX_HIP(hipEventRecord(r.a, s));
         recs.push_back(r);
         return recs.size() - 1;
     }
-    void end(size_t i, hipStream_t s) { NPGX_HIP(hipEventRecord(recs[i].b, s)); }
+    void end(size_t i, hipStream_t s) {
+        if (on) NPGX_HIP(hipEventRecord(recs[i].b, s));
+    }
     int copy_out(npgx_kernel_time* out, int32_t cap, int32_t* n) const {
         int32_t k = 0;
         for (const Rec& r : recs) {

@@ -604,7 +604,7 @@ static void dp_run(npgx_dp* D, const char* first, const int64_t* first_off, cons
         NPGX_HIP(hipMemcpyAsync(D->res.data(), D->d_res.p, (size_t)n * RES * 4, hipMemcpyDeviceToHost, st));
         if (oc) NPGX_HIP(hipMemcpyAsync(raw.data(), D->d_ops.p, (size_t)oc, hipMemcpyDeviceToHost, st));
     }
-    NPGX_HIP(hipStreamSynchronize(st));
+    NPGX_HIP(stream_wait(st));
     D->pinned.reset();
     D->ops.clear();
     for (int32_t i = 0; i < n; i++) {

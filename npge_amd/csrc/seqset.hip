@@ -103,6 +103,12 @@ __global__ void k_pack(const unsigned char* __restrict__ ascii, const int64_t* _
 
 namespace npgx {
 
+hipError_t stream_wait(hipStream_t s) {
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
+    return e;
+}
+
 HostPool::HostPool(int threads) {
     for (int i = 1; i < threads; i++) workers_.emplace_back([this] { loop(); });
 }

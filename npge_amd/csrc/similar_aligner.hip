@@ -1515,7 +1515,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
         al->host_ms[0] += ms(tp);
         tp = std::chrono::steady_clock::now();
-        NPGX_HIP(hipStreamSynchronize(st));
+        NPGX_HIP(stream_wait(st));
         al->host_ms[1] += ms(tp);
         tp = std::chrono::steady_clock::now();
         memcpy(jlen.data(), pl, n_jobs * 4);
@@ -1607,7 +1607,7 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
         NPGX_HIP(hipGetLastError());
         al->timer.end(tg, st);
         NPGX_HIP(hipMemcpyAsync(al->out.data(), al->d_out.p, (size_t)tot, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipStreamSynchronize(st));
+        NPGX_HIP(stream_wait(st));
     }
     al->has_result = true;
 }

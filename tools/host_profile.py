@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Host-side sampling profile of the block build (diagnostic; GPU box):
+SIGPROF sampling inside libnpge_amd.so (npge_amd/csrc/host_sampler.cpp)
+during a few DraftPangenome steps; prints the hottest library functions.
+usage: host_profile.py [config] [steps]"""
+import collections
+import ctypes
+import os
+import subprocess
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from npge_amd import _capi, pipeline, synth  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+L = _capi.lib()
+_capi.check(L.npgx_set_device(0))
+names, seqs = synth.genome_set(cfg)
+ss = _capi.SeqSet(seqs, names)
+job = pipeline.BlockBuild(ss, names, seqs)
+job.run()
+out = os.path.abspath("gpurun_out/host_prof_%s.txt" % cfg)
+os.makedirs(os.path.dirname(out), exist_ok=True)
+L.npgx_diag_prof_start(4000)
+for _ in range(steps):
+    job.run()
+L.npgx_diag_prof_stop(out.encode())
+syms = []
+for line in subprocess.check_output(["nm", "-C", "--defined-only", "-n", _capi.LIB_PATH]).decode().splitlines():
+    parts = line.split(None, 2)
+    if len(parts) == 3 and parts[1].lower() in "tw":
+        syms.append((int(parts[0], 16), parts[2]))
+import bisect
+addrs = [a for a, _ in syms]
+agg = collections.Counter()
+total = 0
+for line in open(out):
+    if line.startswith("#"):
+        total = int(line.split()[-1])
+        continue
+    if line.startswith("lib "):
+        parts = line.split()
+        agg["[" + os.path.basename(" ".join(parts[1:-1])) + "]"] += int(parts[-1])
+        continue
+    off, n = line.split()
+    i = bisect.bisect_right(addrs, int(off, 16)) - 1
+    agg[syms[i][1][:110] if i >= 0 else "?"] += int(n)
+print("samples", total)
+for name, n in agg.most_common(45):
+    print("%6.2f%%  %s" % (100.0 * n / max(total, 1), name))

@@ -92,6 +92,29 @@ struct DevBuf {
     T* grow(size_t n) { return ensure(n > cap ? std::max(n, cap + cap / 2) : n); }
 };
 
+// Pinned host buffer that only grows.
+template <class T>
+struct PinnedBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    T* ensure(size_t n) {
+        if (n == 0) n = 1;
+        if (n > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = std::max(n, cap + cap / 2);
+            NPGX_HIP(hipHostMalloc((void**)&p, cap * sizeof(T), hipHostMallocDefault));
+        }
+        return p;
+    }
+};
+
 // Pinned host staging for async copies (bump allocated; when full, the stream
 // is synchronised so every earlier copy from it has completed).
 struct PinnedArena {

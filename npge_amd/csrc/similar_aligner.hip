@@ -1189,6 +1189,12 @@ struct npgx_aligner {
     npgx_align_options opt;
     int device = 0;
     hipStream_t stream = nullptr;
+    // align_device's host arrays (kept for their capacity)
+    std::vector<npgx::SaJob> h_jobs;
+    std::vector<int64_t> h_ne_off;
+    std::vector<int32_t> h_ne_len, h_order, h_jlen, h_jstat;
+    std::vector<double> h_cost;
+    std::vector<uint8_t> h_cls;
     DevBuf<char> d_rows;
     DevBuf<int64_t> d_row_off;
     DevBuf<int32_t> d_row_len;
@@ -1248,11 +1254,16 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     NPGX_REQUIRE(n_jobs >= 0, NPGX_ERR_ARG, "n_jobs < 0");
     const int64_t r_base = n_jobs ? job_row_start[0] : 0;
     const int64_t n_rows = n_jobs ? (int64_t)job_row_start[n_jobs] - r_base : 0;
-    std::vector<SaJob> jobs(n_jobs);
-    std::vector<int64_t> ne_off;
-    std::vector<int32_t> ne_len;
+    // host arrays kept in the handle across calls (capacity reused)
+    std::vector<SaJob>& jobs = al->h_jobs;
+    std::vector<int64_t>& ne_off = al->h_ne_off;
+    std::vector<int32_t>& ne_len = al->h_ne_len;
+    jobs.resize(n_jobs);
+    ne_off.clear();
+    ne_len.clear();
     res.row_ne.assign((size_t)std::max<int64_t>(n_rows, 1), -1);
-    std::vector<double> cost(n_jobs);
+    std::vector<double>& cost = al->h_cost;
+    cost.resize(n_jobs);
     int64_t scratch = 0, n_reg = 0, n_sub_max = 0;
     int max_n = 1, max_len = 1, max_cap = 1;
     const int wf = weight_factor(o.min_identity_x1e4);
@@ -1298,10 +1309,12 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     }
     // heaviest first (rows x residues), by power-of-two cost classes: the order
     // only balances the load, results do not depend on it
-    std::vector<int32_t> order(n_jobs);
+    std::vector<int32_t>& order = al->h_order;
+    order.resize(n_jobs);
     {
         int cnt[65] = {0};
-        std::vector<uint8_t> cls(n_jobs);
+        std::vector<uint8_t>& cls = al->h_cls;
+        cls.resize(n_jobs);
         for (int32_t j = 0; j < n_jobs; j++) {
             const uint64_t c = (uint64_t)cost[j];
             cls[j] = (uint8_t)(c ? 64 - __builtin_clzll(c) : 0);  // 0..64
@@ -1335,7 +1348,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
     Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
 
-    std::vector<int32_t> jlen(n_jobs), jstat(n_jobs);
+    std::vector<int32_t>& jlen = al->h_jlen;
+    std::vector<int32_t>& jstat = al->h_jstat;
+    jlen.resize(n_jobs);
+    jstat.resize(n_jobs);
     std::vector<int64_t> jst(al->want_stats ? (size_t)n_jobs * NPGX_JOB_STATS : 0);
     res.len.assign(n_jobs, 0);
     res.cap.assign(n_jobs, 0);

@@ -950,9 +950,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
         w.act = lane < n;
         const int cap = job.cap;
-        char* A = (char*)(a.scratch + job.scratch);
+        char* const gA = (char*)(a.scratch + job.scratch);  // the job's global A|B|C
+        char* A = gA;
         char* B = A + (size_t)n * cap;
         char* C = B + (size_t)n * cap;
+        int sb = a.stage_bytes;  // stage bytes free for segments / region arrays
+        bool lds_abc = false;
         View v0{nullptr, 0, 1};
         if (w.act) {
             v0.p = a.rows + a.row_off[job.row0 + lane];
@@ -967,7 +970,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 if (lane == r) off = tot;
                 tot += lr;
             }
-            if (tot <= a.stage_bytes) {
+            // short jobs (no deferred sub-jobs) also keep A|B|C in LDS, at the
+            // end of the stage: the walk's writes and fix_bad_regions /
+            // realing_end / remove_gaps then never leave the CU; the result is
+            // copied to the global A or B at the end
+            const int abc = 3 * n * cap;
+            if ((a.defer == 0 || cap < a.defer) && ((tot + 15) & ~15) + abc <= a.stage_bytes) {
+                lds_abc = true;
+                sb = (a.stage_bytes - abc) & ~15;
+                A = stage + sb;
+                B = A + (size_t)n * cap;
+                C = B + (size_t)n * cap;
+            }
+            if (tot <= sb) {
                 for (int r = 0; r < n; r++) {
                     const char* src = bcast_ptr(v0.p, r);
                     const int lr = bcast(v0.len, r), o = bcast(off, r);
@@ -1021,7 +1036,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 const bool fast = R >= 0;
                 bool counted = false;  // S.regions[].w holds each region's identical columns
                 if (!fast) {
-                    R = regions_in_lds(w, A, cap, L0, a.P.wf, a.P.min_length, stage, a.stage_bytes, S.regions);
+                    R = regions_in_lds(w, A, cap, L0, a.P.wf, a.P.min_length, stage, sb, S.regions);
                     counted = R >= 0;
                     if (R < 0) {
                         count_equal_cols(w, A, cap, 0, L0, S.good_col);
@@ -1078,7 +1093,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
                         before = wave_sum(before);
                     }
-                    const View cv = stage_segment(w, A, cap, C, stage, a.stage_bytes, rg.x, rg.y + 1);
+                    const View cv = stage_segment(w, A, cap, C, stage, sb, rg.x, rg.y + 1);
                     const int Lc = pr.run(cv, colB);
                     if (any_lane(w, pr.ovf)) {
                         ovf = true;
@@ -1103,7 +1118,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 int prefix = L - a.P.ac;
                 if (prefix < 1) prefix = 1;
                 if (!deferred && !ovf && L >= 2 && !tail_identical(w, B, cap, prefix, L)) {
-                    const View tv = stage_segment(w, B, cap, C, stage, a.stage_bytes, prefix, L);
+                    const View tv = stage_segment(w, B, cap, C, stage, sb, prefix, L);
                     const int Lt = pr.run(tv, prefix);
                     if (any_lane(w, pr.ovf)) ovf = true;
                     else {
@@ -1127,6 +1142,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         // 4. remove pure-gap columns
         const long long t_rg = clock64();
         if (!ovf && !deferred) L = remove_pure_gap_cols(w, B, cap, L);
+        if (lds_abc && !ovf) {  // the result to where the host reads it (A for status 2, else B)
+            __syncthreads();
+            char* dst = gA + (B == A ? 0 : (size_t)n * cap);
+            for (int r = 0; r < n; r++)
+                for (int c = lane; c < L; c += 64) dst[(size_t)r * cap + c] = B[(size_t)r * cap + c];
+            __syncthreads();
+        }
         if (lane == 0) {
             a.job_len[j] = ovf ? 0 : L;
             a.job_status[j] = ovf ? 1 : deferred ? 3 : (B == A ? 2 : 0);  // 2: the rows are in A, 3: deferred
@@ -1502,7 +1524,17 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         const int64_t ltab = 1ll << A.ltab_log2;
         const int table_bytes = (int)(16 * ltab + 8 * ((ltab + 1) / 2) + words_bytes);
         const int64_t stage_cap = std::max<int64_t>(0, budget - table_bytes);
-        A.stage_bytes = o.aligner_type == 0 ? (int32_t)std::min<int64_t>((max_rows + 15) & ~15ll, stage_cap & ~15ll) : 0;
+        // short jobs keep A|B|C in the stage too (k_align_jobs): size the stage
+        // for the largest such job within the budget
+        int64_t max_need = (max_rows + 15) & ~15ll;
+        for (int32_t j : todo) {
+            if (A.defer != 0 && jobs[j].cap >= A.defer) continue;
+            int64_t t = 0;
+            for (int i = 0; i < jobs[j].n; i++) t += ne_len[jobs[j].row0 + i];
+            const int64_t need = ((t + 15) & ~15ll) + 3ll * jobs[j].n * jobs[j].cap;
+            if (need <= stage_cap) max_need = std::max(max_need, need);
+        }
+        A.stage_bytes = o.aligner_type == 0 ? (int32_t)std::min<int64_t>(max_need, stage_cap & ~15ll) : 0;
         const size_t lds_bytes = (size_t)table_bytes + (size_t)A.stage_bytes;
         NPGX_REQUIRE(A.stage_bytes >= 0 && lds_bytes <= (size_t)LDS_PER_CU, NPGX_ERR_STATE, "LDS budget");
         int64_t residues = 0;

@@ -1,0 +1,43 @@
+"""bench.py's multi-rank paths on the GPU box's one GPU: two ranks launched by
+torch.distributed.run with the gloo backend (rehearsal of the driver's RCCL
+runs; ranks share the GPU), replicas and sharded modes.  Checks the JSON
+contract fields and that the sharded line reports one set's bp."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("mode", ["replicas", "sharded"])
+def test_bench_two_ranks_gloo(mode):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--steps", "1", "--warmup", "1", "--config", "small", "--mode", mode,
+           "--dist-backend", "gloo", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    bp = d["config"]["bp_per_rank"]
+    ranks = 1 if mode == "sharded" else 2
+    assert abs(d["value"] - bp * ranks / (d["ms_per_step"] / 1e3) / 1e6) / d["value"] < 1e-3
+    assert d["scaling"] == ("strong" if mode == "sharded" else "weak")

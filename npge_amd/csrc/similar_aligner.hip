@@ -1216,6 +1216,7 @@ struct npgx_aligner {
     std::vector<int64_t> h_ne_off;
     std::vector<int32_t> h_ne_len, h_order, h_jlen, h_jstat;
     std::vector<double> h_cost;
+    std::vector<int32_t> h_jsum;
     std::vector<uint8_t> h_cls;
     DevBuf<char> d_rows;
     DevBuf<int64_t> d_row_off;
@@ -1286,6 +1287,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     res.row_ne.assign((size_t)std::max<int64_t>(n_rows, 1), -1);
     std::vector<double>& cost = al->h_cost;
     cost.resize(n_jobs);
+    std::vector<int32_t>& jsum = al->h_jsum;  // residues per job
+    jsum.resize(n_jobs);
     int64_t scratch = 0, n_reg = 0, n_sub_max = 0;
     int max_n = 1, max_len = 1, max_cap = 1;
     const int wf = weight_factor(o.min_identity_x1e4);
@@ -1325,6 +1328,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         n_reg += J.reg_cap;
         n_sub_max += (J.reg_cap + 1) / 2;
         cost[j] = double(n) * double(sum);
+        jsum[j] = (int32_t)std::min<int64_t>(sum, INT32_MAX);
         max_n = std::max(max_n, n);
         max_len = std::max(max_len, mx);
         max_cap = std::max<int>(max_cap, J.cap);
@@ -1504,11 +1508,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // up to half of what is left) and the stage for the job's rows.  The
         // budget shrinks as more workgroups must be resident per CU.
         int64_t max_rows = 0;
-        for (int32_t j : todo) {
-            int64_t t = 0;
-            for (int i = 0; i < jobs[j].n; i++) t += ne_len[jobs[j].row0 + i];
-            max_rows = std::max(max_rows, t);
-        }
+        for (int32_t j : todo) max_rows = std::max<int64_t>(max_rows, jsum[j]);
         const int64_t per_cu = std::min<int64_t>(16, std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
         const int64_t budget = LDS_PER_CU / per_cu;
         // word history of the row-parallel search (HIST_SHIFTS x 64 words) when
@@ -1529,17 +1529,14 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         int64_t max_need = (max_rows + 15) & ~15ll;
         for (int32_t j : todo) {
             if (A.defer != 0 && jobs[j].cap >= A.defer) continue;
-            int64_t t = 0;
-            for (int i = 0; i < jobs[j].n; i++) t += ne_len[jobs[j].row0 + i];
-            const int64_t need = ((t + 15) & ~15ll) + 3ll * jobs[j].n * jobs[j].cap;
+            const int64_t need = (((int64_t)jsum[j] + 15) & ~15ll) + 3ll * jobs[j].n * jobs[j].cap;
             if (need <= stage_cap) max_need = std::max(max_need, need);
         }
         A.stage_bytes = o.aligner_type == 0 ? (int32_t)std::min<int64_t>(max_need, stage_cap & ~15ll) : 0;
         const size_t lds_bytes = (size_t)table_bytes + (size_t)A.stage_bytes;
         NPGX_REQUIRE(A.stage_bytes >= 0 && lds_bytes <= (size_t)LDS_PER_CU, NPGX_ERR_STATE, "LDS budget");
         int64_t residues = 0;
-        for (int32_t j : todo)
-            for (int i = 0; i < jobs[j].n; i++) residues += ne_len[jobs[j].row0 + i];
+        for (int32_t j : todo) residues += jsum[j];
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
                                     double(residues) * 2.0, residues);
         hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);

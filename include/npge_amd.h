@@ -202,13 +202,13 @@ int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_
 /* per job of the last batch, NPGX_JOB_STATS int64: 0 device cycles,
  * 1 alignment columns, 2 try_aligned calls, 3 shifts scanned, 4 try_gap calls,
  * 5 FindLowSimilar regions, 6 non-empty rows, 7 columns-mode chunks; cycles
- * of 8 process_seqs, 9 fix_bad_regions, 10 realing_end, 11 remove_gaps; and,
+ * of 8 process_seqs, 9 fix_bad_regions, 10 realing_end; 11 wall_clock64() at
+ * the job's start (constant-rate device clock, 23 at its end); and,
  * in a library built with NPGX_SA_PROFILE, cycles inside process_seqs of
  * 12 columns-mode runs, 13 rows-mode equal/mismatch steps, 14 try_gap,
  * 15 try_aligned, 16 vector word building, 17 vector word compares,
  * 18 vector chunks, 19 vector calls, 20 append_end, 21 returns from
- * append_aligned (0 otherwise); 22 cycles of the region search, 23 regions
- * before merging (alignments over 4096 columns) */
+ * append_aligned (0 otherwise); 22 cycles of the region search */
 #define NPGX_JOB_STATS 24
 int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64_t* n);
 void npgx_aligner_free(npgx_aligner* a);

@@ -940,6 +940,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             continue;
         }
         const long long t_job = clock64();
+        const unsigned long long w_job = wall_clock64();  // constant-rate clock, for timelines
         long long t_ph[3] = {0, 0, 0}, st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         long long t_regions = 0;
         int st_regions0 = 0;
@@ -1140,7 +1141,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
         __syncthreads();
         // 4. remove pure-gap columns
-        const long long t_rg = clock64();
         if (!ovf && !deferred) L = remove_pure_gap_cols(w, B, cap, L);
         if (lds_abc && !ovf) {  // the result to where the host reads it (A for status 2, else B)
             __syncthreads();
@@ -1164,10 +1164,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             js[8] = t_ph[0];
             js[9] = t_ph[1];
             js[10] = t_ph[2];
-            js[11] = clock64() - t_rg;
+            js[11] = (int64_t)w_job;
             for (int q = 0; q < 10; q++) js[12 + q] = st_prof[q];
             js[22] = t_regions;
-            js[23] = st_regions0;
+            js[23] = (int64_t)wall_clock64();
         }
         __syncthreads();
     }

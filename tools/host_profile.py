@@ -34,10 +34,18 @@ for line in subprocess.check_output(["nm", "-C", "--defined-only", "-n", _capi.L
 import bisect
 addrs = [a for a, _ in syms]
 agg = collections.Counter()
+callers = collections.Counter()
 total = 0
 for line in open(out):
     if line.startswith("#"):
         total = int(line.split()[-1])
+        continue
+    if line.startswith("caller "):
+        _, c0, c1, n = line.split()
+        def sym(o):
+            i = bisect.bisect_right(addrs, int(o, 16)) - 1
+            return syms[i][1][:60] if i >= 0 and int(o, 16) else "-"
+        callers["%s  <-  %s" % (sym(c0), sym(c1))] += int(n)
         continue
     if line.startswith("lib "):
         parts = line.split()
@@ -48,4 +56,7 @@ for line in open(out):
     agg[syms[i][1][:110] if i >= 0 else "?"] += int(n)
 print("samples", total)
 for name, n in agg.most_common(45):
+    print("%6.2f%%  %s" % (100.0 * n / max(total, 1), name))
+print("\noutside the library, by calling library function (first %d samples):" % min(total, 65536))
+for name, n in callers.most_common(40):
     print("%6.2f%%  %s" % (100.0 * n / max(total, 1), name))

@@ -267,7 +267,8 @@ typedef struct {
 
 void npgx_bb_default_options(npgx_bb_options* o);
 int npgx_blockset_create(const npgx_seqset* s, const npgx_bb_options* o, npgx_blockset** out);
-/* replace the blocks; row_off == NULL: no rows, else row i = rows[row_off[i]..row_off[i+1]) */
+/* replace the blocks; row_off == NULL: no rows, else row i = rows[row_off[i]..row_off[i+1])
+ * (a block whose rows are all empty is unaligned) */
 int npgx_blockset_set_blocks(npgx_blockset* b, int64_t n_blocks, const int64_t* block_start,
                              const int32_t* seq, const int64_t* min_pos, const int64_t* max_pos,
                              const int8_t* ori, const int64_t* row_off, const char* rows);
@@ -289,6 +290,26 @@ int npgx_blockset_copy(const npgx_blockset* b, int64_t* block_start, int32_t* se
                        char* rows);
 /* blockset_hash (src/model/block_hash.cpp:112-130) */
 int npgx_blockset_hash(const npgx_blockset* b, uint64_t* hash);
+/* ConSeq (replaces ConSeq::process_block_impl, src/algo/ConSeq.cpp:37-50):
+ * the text of the sequence each block becomes, in block order -- one
+ * fragment: its text (FragmentSequence); aligned: Block::consensus
+ * (Block.cpp:147-185, per column the most frequent of A T G C N, first in
+ * that order on ties, 'A' for a column without letters), computed on the
+ * GPU; unaligned: the first longest fragment's text.  Call with out == NULL
+ * for *n_blocks and *total, then with out (total bytes) and out_off
+ * (n_blocks + 1 offsets). */
+int npgx_blockset_conseq(npgx_blockset* b, char* out, int64_t* out_off, int64_t* n_blocks,
+                         int64_t* total);
+/* DeConSeq (replaces DeConSeq::deconseq_block / deconseq_row,
+ * src/algo/DeConSeq.cpp:27-96): every block of `cons` -- a block set over
+ * the sequences npgx_blockset_conseq made of `source`'s blocks (sequence i =
+ * source block i, source unchanged since) -- becomes a block over source's
+ * sequences: each fragment is Block::slice (Block.cpp:238-289) of its source
+ * block at the fragment's consensus columns, aligned fragments compose their
+ * rows.  The new blocks are appended to `target`, whose sequences equal
+ * source's (target may be source).  NPGX_ERR_STATE when cons does not
+ * match source. */
+int npgx_blockset_deconseq(npgx_blockset* target, npgx_blockset* source, npgx_blockset* cons);
 int npgx_blockset_stats(const npgx_blockset* b, npgx_bb_stats* out);
 int npgx_blockset_kernel_times(const npgx_blockset* b, npgx_kernel_time* out, int32_t cap,
                                int32_t* n);

@@ -52,6 +52,8 @@ def _bind(L):
     L.npgx_blockset_counts.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.npgx_blockset_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
     L.npgx_blockset_hash.argtypes = [vp, P(ctypes.c_uint64)]
+    L.npgx_blockset_conseq.argtypes = [vp, vp, vp, P(i64), P(i64)]
+    L.npgx_blockset_deconseq.argtypes = [vp, vp, vp]
     L.npgx_blockset_stats.argtypes = [vp, P(BbStats)]
     L.npgx_blockset_kernel_times.argtypes = [vp, P(_capi.KernelTime), ctypes.c_int32,
                                              P(ctypes.c_int32)]
@@ -106,11 +108,11 @@ class BlockSetEngine:
         mn = np.array([f[1] for f in frs] or [0], dtype=np.int64)
         mx = np.array([f[2] for f in frs] or [0], dtype=np.int64)
         ori = np.array([f[3] for f in frs] or [1], dtype=np.int8)
-        has_rows = bool(frs) and frs[0][4] is not None
-        if has_rows:
-            rows = "".join(f[4] for f in frs).encode()
+        has_rows = any(f[4] is not None for f in frs)
+        if has_rows:  # per block: rows for every fragment, or none (zero-length rows)
+            rows = "".join(f[4] or "" for f in frs).encode()
             ro = np.zeros(len(frs) + 1, dtype=np.int64)
-            np.cumsum([len(f[4]) for f in frs], out=ro[1:])
+            np.cumsum([len(f[4] or "") for f in frs], out=ro[1:])
             buf = ctypes.create_string_buffer(rows, max(len(rows), 1))
             _capi.check(L.npgx_blockset_set_blocks(self._h, len(blocks), _capi.ptr(bs), _capi.ptr(seq),
                                                    _capi.ptr(mn), _capi.ptr(mx), _capi.ptr(ori),
@@ -151,6 +153,29 @@ class BlockSetEngine:
                 blk.append((int(seq[i]), int(mn[i]), int(mx[i]), int(ori[i]), row))
             out.append(blk)
         return out
+
+    def conseq(self):
+        """ConSeq (ConSeq.cpp:37-50): the text of the sequence each block
+        becomes, in block order (consensus of aligned blocks on the GPU)."""
+        L = _bind(_capi.lib())
+        nb, tot = ctypes.c_int64(), ctypes.c_int64()
+        _capi.check(L.npgx_blockset_conseq(self._h, None, None, ctypes.byref(nb), ctypes.byref(tot)))
+        buf = ctypes.create_string_buffer(max(tot.value, 1))
+        off = np.zeros(nb.value + 1, dtype=np.int64)
+        _capi.check(L.npgx_blockset_conseq(self._h, ctypes.cast(buf, ctypes.c_void_p), _capi.ptr(off),
+                                           ctypes.byref(nb), ctypes.byref(tot)))
+        raw = buf.raw
+        return [raw[off[i]:off[i + 1]].decode() for i in range(nb.value)]
+
+    def deconseq(self, cons, source=None):
+        """DeConSeq (DeConSeq.cpp:48-96): the blocks of `cons` (an engine over
+        the sequences conseq() made of `source`'s blocks, sequence i = block i)
+        mapped back onto source's sequences and appended to this engine's
+        blocks; source defaults to this engine."""
+        L = _bind(_capi.lib())
+        src = self if source is None else source
+        _capi.check(L.npgx_blockset_deconseq(self._h, src._h, cons._h))
+        return self
 
     def hash(self):
         h = ctypes.c_uint64()

@@ -19,6 +19,9 @@ class Sequence:
     name: str
     data: str            # after to_atgcn (Sequence.cpp:151-179)
     description: str = ""
+    # the block whose consensus this sequence holds (Sequence::set_block,
+    # Sequence.cpp:301-335; set by ConSeq, read by DeConSeq)
+    block: Optional["Block"] = field(default=None, repr=False, compare=False)
 
     def size(self):
         return len(self.data)

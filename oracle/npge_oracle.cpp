@@ -27,6 +27,7 @@
 #include <map>
 #include <set>
 #include <tuple>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -1266,6 +1267,196 @@ static int fix_ends(const std::vector<BSeq>& seqs, const BBlock& b, int min_frag
 }
 
 // ---------------------------------------------------------------- Filter
+// ---------------------------------------------------------------- ConSeq / DeConSeq
+// A gapped row as the reference's AlignmentRow sees it: column -> fragment
+// position (-1 = gap) and back (AlignmentRow.hpp:40-120).
+struct RowMap {
+    std::vector<int64_t> a2f, f2a;
+    explicit RowMap(const std::string& row) : a2f(row.size(), -1) {
+        for (size_t c = 0; c < row.size(); c++)
+            if (row[c] != '-') {
+                a2f[c] = (int64_t)f2a.size();
+                f2a.push_back((int64_t)c);
+            }
+    }
+    int64_t length() const { return (int64_t)a2f.size(); }
+    int64_t map_to_fragment(int64_t col) const { return col >= 0 && col < length() ? a2f[(size_t)col] : -1; }
+    int64_t map_to_alignment(int64_t pos) const {
+        return pos >= 0 && pos < (int64_t)f2a.size() ? f2a[(size_t)pos] : -1;
+    }
+    // AlignmentRow::nearest_in_fragment_impl (AlignmentRow.cpp:101-112): left first
+    int64_t nearest_in_fragment(int64_t col) const {
+        for (int64_t d = 0; d <= length(); d++)
+            for (int o = -1; o <= 1; o += 2) {
+                const int64_t p = map_to_fragment(col + o * d);
+                if (p != -1) return p;
+            }
+        return -1;
+    }
+};
+
+// the row string of fragment f (letters = f's text in its orientation) for
+// the fragment positions bound at columns: bound[col] = position or -1
+static std::string row_from_binding(const std::vector<BSeq>& seqs, const BFrag& f,
+                                    const std::vector<int64_t>& bound) {
+    const std::string t = frag_text(seqs, f);
+    std::string r(bound.size(), '-');
+    for (size_t c = 0; c < bound.size(); c++)
+        if (bound[c] >= 0) {
+            if ((size_t)bound[c] >= t.size()) throw std::runtime_error("row binds a position past the fragment");
+            r[c] = t[(size_t)bound[c]];
+        }
+    return r;
+}
+
+// Block::alignment_length (Block.cpp:133-139)
+static int64_t block_alignment_length(const BBlock& b) {
+    int64_t r = 0;
+    for (const BFrag& f : b.f) r = std::max<int64_t>(r, f.has_row ? (int64_t)f.row.size() : f.length());
+    return r;
+}
+
+// Block::consensus (Block.cpp:147-185): unaligned -> the first longest
+// fragment's text; aligned -> consensus_char per column: counts of the letters
+// (test_column, block_stat.cpp:188-210, char_to_size index < LETTERS_NUMBER = 5,
+// i.e. A T G C N), the first letter in that order with the highest count
+// (a column without letters: every count is 0 = the maximum -> 'A')
+static std::string consensus(const std::vector<BSeq>& seqs, const BBlock& b) {
+    if (b.f.empty()) return std::string();
+    if (!b.f[0].has_row) {
+        const BFrag* longest = &b.f[0];
+        for (const BFrag& f : b.f)
+            if (f.length() > longest->length()) longest = &f;
+        return frag_text(seqs, *longest);
+    }
+    const int64_t L = block_alignment_length(b);
+    std::string out((size_t)L, ' ');
+    for (int64_t c = 0; c < L; c++) {
+        int freq[5] = {0, 0, 0, 0, 0};
+        for (const BFrag& f : b.f) {
+            const char x = c < (int64_t)f.row.size() ? f.row[(size_t)c] : '-';  // alignment_at: 0 = gap
+            if (x != '-') {
+                const size_t li = char_to_size(x);
+                if (li < 5) freq[li]++;
+            }
+        }
+        int mx = 0;
+        for (int l = 0; l < 5; l++) mx = std::max(mx, freq[l]);
+        int l = 0;
+        while (freq[l] != mx) l++;
+        out[(size_t)c] = "ATGCN"[l];
+    }
+    return out;
+}
+
+// ConSeq::process_block_impl (ConSeq.cpp:37-50): one fragment -> the fragment
+// itself (FragmentSequence), two or more -> Block::consensus
+static std::string conseq_text(const std::vector<BSeq>& seqs, const BBlock& b) {
+    if (b.f.size() == 1) return frag_text(seqs, b.f[0]);
+    return consensus(seqs, b);
+}
+
+// proportion.hpp:16-23
+static int64_t proportion(int64_t part1, int64_t total1, int64_t total2) {
+    if (total1 == 0) return 0;
+    const double percentage = double(part1) / double(total1);
+    return (int64_t)(int)(percentage * (double)total2 + 0.00000001);
+}
+
+// fragment_pos (convert_position.cpp:44-67)
+static int64_t fragment_pos(const BFrag& f, int64_t block_pos, int64_t block_length) {
+    if (f.has_row) {
+        int64_t r = RowMap(f.row).nearest_in_fragment(block_pos);
+        if (r == -1) r = block_pos < block_length / 2 ? 0 : f.length();
+        return r;
+    }
+    return proportion(block_pos, block_length, f.length());
+}
+
+// Fragment::set_begin_last (Fragment.cpp:117-127)
+static void set_begin_last(BFrag& f, int64_t b, int64_t l) {
+    if (b <= l) {
+        f.min = b;
+        f.max = l;
+        f.ori = 1;
+    } else {
+        f.min = l;
+        f.max = b;
+        f.ori = -1;
+    }
+}
+
+// Block::slice (Block.cpp:238-289) with AlignmentRow::slice (AlignmentRow.cpp:153-171)
+static BBlock block_slice_full(const std::vector<BSeq>& seqs, const BBlock& b, int64_t start, int64_t stop,
+                               bool alignment) {
+    const int64_t bl = block_alignment_length(b);
+    const int64_t mn = std::min(start, stop), mx = std::max(start, stop);
+    const int ori = mn == start ? 1 : -1;
+    BBlock r;
+    for (const BFrag& f : b.f) {
+        int64_t fs = fragment_pos(f, start, bl), fe = fragment_pos(f, stop, bl);
+        if (f.has_row) {
+            const RowMap m(f.row);
+            const int64_t a = m.map_to_alignment(fs);
+            if (a < mn || a > mx) fs += ori;
+            const int64_t z = m.map_to_alignment(fe);
+            if (z < mn || z > mx) fe -= ori;
+        }
+        if ((fe - fs) * ori < 0) continue;  // empty sub-fragment
+        BFrag nf;
+        nf.seq = f.seq;
+        set_begin_last(nf, f.begin() + f.ori * fs, f.begin() + f.ori * fe);  // frag_to_seq
+        if (alignment) {
+            nf.has_row = true;
+            if (f.has_row) {
+                const RowMap m(f.row);
+                std::vector<int64_t> bound((size_t)(mx - mn + 1), -1);
+                int64_t fp = 0;
+                for (int64_t c = 0; c < (int64_t)bound.size(); c++)
+                    if (m.map_to_fragment(start + c * ori) != -1) bound[(size_t)c] = fp++;
+                nf.row = row_from_binding(seqs, nf, bound);
+            } else {
+                nf.row = frag_text(seqs, nf);  // CompactAlignmentRow(new_fragment->str())
+            }
+        }
+        r.f.push_back(nf);
+    }
+    return r;
+}
+
+// deconseq_row (DeConSeq.cpp:27-46): column i of the consensus fragment's row
+// -> its fragment position -> the position bound there in the sliced row
+static void deconseq_row(const std::vector<BSeq>& seqs, const BFrag& cons, BFrag& f) {
+    const RowMap row(cons.row), tmp(f.row);
+    std::vector<int64_t> bound((size_t)row.length(), -1);
+    for (int64_t i = 0; i < row.length(); i++) {
+        const int64_t tp = row.map_to_fragment(i);
+        if (tp != -1) {
+            const int64_t np = tmp.map_to_fragment(tp);
+            if (np != -1) bound[(size_t)i] = np;
+        }
+    }
+    f.row = row_from_binding(seqs, f, bound);
+}
+
+// DeConSeq::deconseq_block (DeConSeq.cpp:48-74): every fragment of a block
+// over consensus sequences (sequence i = source block i) becomes the slice of
+// that source block at the fragment's columns
+static BBlock deconseq_block(const std::vector<BSeq>& seqs, const std::vector<BBlock>& source,
+                             const BBlock& cb) {
+    BBlock nb;
+    nb.name = cb.name;
+    for (const BFrag& cf : cb.f) {
+        const BBlock& sb = source.at((size_t)cf.seq);
+        BBlock t = block_slice_full(seqs, sb, cf.begin(), cf.last(), cf.has_row);
+        for (BFrag& f : t.f) {
+            if (f.has_row) deconseq_row(seqs, cf, f);
+            nb.f.push_back(f);
+        }
+    }
+    return nb;
+}
+
 static const int MAX_COLUMN_SCORE = 100;
 static const int LOG_SCORE[1000] = {
 #include "log_score.inc"
@@ -2012,5 +2203,39 @@ void orc_bs_copy(const orc_bs* h, int64_t* block_start, int32_t* seq, int64_t* m
 }
 
 uint64_t orc_bs_hash(const orc_bs* h) { return orc::blockset_hash(h->bs); }
+
+// ConSeq: the text of the sequence each block becomes (in block order), two
+// calls: total size (out == NULL), then the bytes and n_blocks + 1 offsets
+int64_t orc_bs_conseq(const orc_bs* h, char* out, int64_t* off) {
+    int64_t t = 0;
+    for (size_t b = 0; b < h->bs.blocks.size(); b++) {
+        const std::string s = orc::conseq_text(h->seqs, h->bs.blocks[b]);
+        if (off) off[b] = t;
+        if (out) memcpy(out + t, s.data(), s.size());
+        t += (int64_t)s.size();
+    }
+    if (off) off[h->bs.blocks.size()] = t;
+    return t;
+}
+
+// DeConSeq: the blocks of `cons` (over the sequences orc_bs_conseq made from
+// `source`'s blocks) mapped onto source's sequences, appended to target's
+// blocks (target and source share their sequences); -1 on a mismatch
+int orc_bs_deconseq(orc_bs* target, const orc_bs* source, const orc_bs* cons) {
+    if (cons->seqs.size() != source->bs.blocks.size()) return -1;
+    std::vector<orc::BBlock> out;
+    for (const auto& cb : cons->bs.blocks) {
+        for (const auto& cf : cb.f)
+            if (cf.seq < 0 || (size_t)cf.seq >= source->bs.blocks.size()) return -1;
+        try {
+            orc::BBlock nb = orc::deconseq_block(source->seqs, source->bs.blocks, cb);
+            if (!nb.f.empty()) out.push_back(nb);
+        } catch (const std::exception&) {
+            return -2;
+        }
+    }
+    for (auto& b : out) target->bs.blocks.push_back(b);
+    return 0;
+}
 
 }  // extern "C"

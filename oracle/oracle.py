@@ -269,6 +269,10 @@ def _bs_lib():
         L.orc_bs_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orc_bs_hash.argtypes = [vp]
         L.orc_bs_hash.restype = ctypes.c_uint64
+        L.orc_bs_conseq.argtypes = [vp, vp, vp]
+        L.orc_bs_conseq.restype = i64
+        L.orc_bs_deconseq.argtypes = [vp, vp, vp]
+        L.orc_bs_deconseq.restype = ctypes.c_int
         L._bs_bound = True
     return L
 
@@ -353,3 +357,24 @@ class BlockSetOracle:
 
     def hash(self):
         return _bs_lib().orc_bs_hash(self._h)
+
+    def conseq(self):
+        """ConSeq (ConSeq.cpp:37-50): the sequence text each block becomes."""
+        L = _bs_lib()
+        n = len(self.blocks())
+        tot = L.orc_bs_conseq(self._h, None, None)
+        buf = ctypes.create_string_buffer(max(tot, 1))
+        off = np.zeros(n + 1, dtype=np.int64)
+        L.orc_bs_conseq(self._h, ctypes.cast(buf, ctypes.c_void_p), _ptr(off))
+        raw = buf.raw
+        return [raw[off[i]:off[i + 1]].decode() for i in range(n)]
+
+    def deconseq(self, cons, source=None):
+        """DeConSeq (DeConSeq.cpp:48-96): blocks of `cons` (an oracle over the
+        sequences conseq() made from `source`'s blocks, sequence i = block i)
+        mapped back and appended to this set's blocks."""
+        src = self if source is None else source
+        rc = _bs_lib().orc_bs_deconseq(self._h, src._h, cons._h)
+        if rc != 0:
+            raise RuntimeError("oracle DeConSeq failed (%d)" % rc)
+        return self

@@ -13,6 +13,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NPGX_PROFILE=1 selects the diagnostic build with aligner cycle counters
 LIB_PATH = os.path.join(_HERE, "libnpge_amd_prof.so" if os.environ.get("NPGX_PROFILE") == "1"
                         else "libnpge_amd.so")
+# NPGX_LIB=<file in npge_amd/>: an alternate build of the same library (A/B timing)
+if os.environ.get("NPGX_LIB"):
+    LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ["NPGX_LIB"]))
 
 NPGX_OK = 0
 ERRORS = {-1: "NPGX_ERR_ARG", -2: "NPGX_ERR_HIP", -3: "NPGX_ERR_NODEV", -4: "NPGX_ERR_RANGE",

@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/B timing of two builds of the library on one box (diagnostic):
+#   tools/ab_bench.sh <alt .so in npge_amd/> [rounds] [extra bench args]
+# alternates bench.py runs with the default library and NPGX_LIB=<alt>.
+ALT=$1; N=${2:-3}; shift 2
+mkdir -p gpurun_out
+for i in $(seq 1 $N); do
+  for v in new alt; do
+    if [ $v = alt ]; then export NPGX_LIB=$ALT; else unset NPGX_LIB; fi
+    timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
+    python - "$v" <<'PY'
+import json, sys
+d = json.loads(open("gpurun_out/ab_%s.log" % sys.argv[1]).read().strip().splitlines()[-1])
+s = d["last_step"]["ms_stage"]
+print(sys.argv[1], d["ms_per_step"], {k: s[k] for k in ("overlapless_union", "ou_order", "ou_admit", "align_batch", "fix_ends", "filter")})
+PY
+  done
+done

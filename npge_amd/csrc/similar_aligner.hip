@@ -1033,7 +1033,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 int4 rreg = make_int4(0, 0, 0, 0);
                 unsigned long long gmask = 0;
                 const long long t_reg0 = clock64();
-                int R = regions_in_registers(w, A, cap, L0, a.P.wf, a.P.min_length, rreg, gmask, (int*)S.good_col);
+                // 64 ints of scratch: the row stage (its rows are dead after
+                // process_seqs) when it has room, else the slot's global area
+                int* rtmp = sb >= 256 ? (int*)stage : (int*)S.good_col;
+                int R = regions_in_registers(w, A, cap, L0, a.P.wf, a.P.min_length, rreg, gmask, rtmp);
                 const bool fast = R >= 0;
                 bool counted = false;  // S.regions[].w holds each region's identical columns
                 if (!fast) {
@@ -1152,6 +1155,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (lane == 0) {
             a.job_len[j] = ovf ? 0 : L;
             a.job_status[j] = ovf ? 1 : deferred ? 3 : (B == A ? 2 : 0);  // 2: the rows are in A, 3: deferred
+        }
+        if (lane == 0 && a.job_stats) {  // only when the statistics are wanted
             int64_t* js = a.job_stats + (size_t)j * NPGX_JOB_STATS;
             js[0] = clock64() - t_job;
             js[1] = L;
@@ -1445,7 +1450,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.scratch = scr.p;
         A.job_len = al->d_job_len.p;
         A.job_status = al->d_job_status.p;
-        A.job_stats = al->d_job_stats.p;
+        A.job_stats = al->want_stats ? al->d_job_stats.p : nullptr;
         A.next_job = al->d_next.p;
         A.tkeys = al->tkeys.p;
         A.tmask = al->tmask.p;

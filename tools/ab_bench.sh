@@ -12,7 +12,7 @@ for i in $(seq 1 $N); do
 import json, sys
 d = json.loads(open("gpurun_out/ab_%s.log" % sys.argv[1]).read().strip().splitlines()[-1])
 s = d["last_step"]["ms_stage"]
-print(sys.argv[1], d["ms_per_step"], {k: s[k] for k in ("overlapless_union", "ou_order", "ou_admit", "align_batch", "fix_ends", "filter")})
+print(sys.argv[1], d["ms_per_step"], " ".join("%s=%.2f" % (k[:8], v) for k, v in s.items()))
 PY
   done
 done

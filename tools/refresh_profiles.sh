@@ -21,6 +21,11 @@ tail -1 $O/bench_c2.log | cut -c1-400
 step bench_c3
 timeout -k 10 600 python bench.py --config C3 --cpu-sample C3 --steps 5 --warmup 2 > $O/bench_c3.log 2>&1 || { tail -5 $O/bench_c3.log; exit 1; }
 tail -1 $O/bench_c3.log | cut -c1-300
+step bench_c4
+timeout -k 10 600 python bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_c4.log 2>&1 || { tail -5 $O/bench_c4.log; exit 1; }
+tail -1 $O/bench_c4.log | cut -c1-300
+step timeline
+timeout -k 10 300 python tools/align_timeline.py C2 > $O/align_timeline_c2.txt 2>&1 || { tail -5 $O/align_timeline_c2.txt; exit 1; }
 step bench_dp
 timeout -k 10 600 python tools/bench_dp.py > $O/bench_dp.log 2>&1 || { tail -5 $O/bench_dp.log; exit 1; }
 tail -1 $O/bench_dp.log | cut -c1-300

@@ -87,6 +87,7 @@ struct SaArgs {
     Params P;
     // deferred fix_bad_regions (attempt 0): regions and sub-jobs
     int32_t defer;             // > 0: defer the bad regions of alignments of at least this many columns
+    int32_t defer_rows;        // ... and at least this many rows
     int4* job_regions;         // per job: x, y, good (1) or -(sub+1), identical columns before
     int32_t* job_nreg;         // regions per deferred job
     SaSub* subs;
@@ -976,7 +977,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             // realing_end / remove_gaps then never leave the CU; the result is
             // copied to the global A or B at the end
             const int abc = 3 * n * cap;
-            if ((a.defer == 0 || cap < a.defer) && ((tot + 15) & ~15) + abc <= a.stage_bytes) {
+            const bool may_defer = a.defer != 0 && cap >= a.defer && n >= a.defer_rows;
+            if (!may_defer && ((tot + 15) & ~15) + abc <= a.stage_bytes) {
                 lds_abc = true;
                 sb = (a.stage_bytes - abc) & ~15;
                 A = stage + sb;
@@ -1053,7 +1055,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 t_regions = clock64() - t_reg0;
                 st_regions = R;
                 int colB = 0;
-                if (a.defer && L0 >= a.defer && !(fast && R == 1 && bcast(rreg.z, 0)))
+                if (a.defer && L0 >= a.defer && n >= a.defer_rows && !(fast && R == 1 && bcast(rreg.z, 0)))
                     deferred = defer_regions(DeferOut{a.job_regions, a.job_nreg, a.subs, a.alloc, a.counters,
                                                       a.pool, a.pool_cap, a.max_sub, a.fin},
                                              n, j, job.reg_off, job.reg_cap, A, C, cap, R, fast, counted, rreg,
@@ -1248,7 +1250,12 @@ struct npgx_aligner {
     // deferred fix_bad_regions (first attempt)
     // NPGX_ALIGN_DEFER=<columns>: alignments at least this long hand their bad
     // regions to k_align_sub (0: every bad region realigned inside its job)
-    int defer = 1000;
+    // deferred bad regions (sub-jobs of their own): alignments of at least
+    // this many columns and rows -- long many-row alignments gain (C3 17 rows:
+    // align 46.6 -> 45.0 ms at 8000 vs 1000 columns), 3-row ones only pay the
+    // extra launches (C2 align 11.1 -> 10.4 ms without)
+    int defer = 8000;
+    int defer_rows = 4;
     DevBuf<int4> d_job_regions;
     DevBuf<int32_t> d_job_nreg, d_fin;
     DevBuf<SaSub> d_subs;
@@ -1467,8 +1474,13 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.good_col = al->good_col.p;
         A.slot_cols = slot_cols;
         A.P = P;
-        const bool defer = attempt == 0 && al->defer > 0 && o.aligner_type == 0 && n_reg > 0 && max_cap >= al->defer;
+        bool defer = attempt == 0 && al->defer > 0 && o.aligner_type == 0 && n_reg > 0 && max_cap >= al->defer;
+        if (defer) {  // some job long enough and with enough rows
+            defer = false;
+            for (int32_t j : todo) defer |= jobs[j].cap >= al->defer && jobs[j].n >= al->defer_rows;
+        }
         A.defer = defer ? al->defer : 0;
+        A.defer_rows = al->defer_rows;
         if (defer) {
             al->d_job_regions.grow((size_t)n_reg);
             al->d_job_nreg.grow(jobs.size());
@@ -1533,7 +1545,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // for the largest such job within the budget
         int64_t max_need = (max_rows + 15) & ~15ll;
         for (int32_t j : todo) {
-            if (A.defer != 0 && jobs[j].cap >= A.defer) continue;
+            if (A.defer != 0 && jobs[j].cap >= A.defer && jobs[j].n >= A.defer_rows) continue;
             const int64_t need = (((int64_t)jsum[j] + 15) & ~15ll) + 3ll * jobs[j].n * jobs[j].cap;
             if (need <= stage_cap) max_need = std::max(max_need, need);
         }
@@ -1708,6 +1720,8 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         a->want_stats = js && js[0] == '1';
         const char* df = getenv("NPGX_ALIGN_DEFER");
         if (df && *df) a->defer = std::max(0, atoi(df));
+        const char* dr = getenv("NPGX_ALIGN_DEFER_ROWS");
+        if (dr && *dr) a->defer_rows = std::max(0, atoi(dr));
         if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
             delete a;
             throw Error(NPGX_ERR_HIP, "stream creation failed");

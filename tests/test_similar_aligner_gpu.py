@@ -114,21 +114,24 @@ def test_random_families(seed):
     _check(_random_jobs(seed, 150))
 
 
-# NPGX_ALIGN_DEFER (read when the aligner is created): the column count from
+# NPGX_ALIGN_DEFER / NPGX_ALIGN_DEFER_ROWS (read when the aligner is created):
+# the column and row counts from
 # which fix_bad_regions' re-alignments leave the job's workgroup and run as
 # sub-jobs of their own (0: never, 1: every alignment)
-@pytest.mark.parametrize("defer", ["0", "1", "1000"])
-def test_long_flanks(defer, monkeypatch):
+@pytest.mark.parametrize("defer,rows", [("0", "0"), ("1", "0"), ("1000", "0"), ("1000", "4"), ("8000", "4")])
+def test_long_flanks(defer, rows, monkeypatch):
     monkeypatch.setenv("NPGX_ALIGN_DEFER", defer)
+    monkeypatch.setenv("NPGX_ALIGN_DEFER_ROWS", rows)  # deferred only with at least this many rows
     _check(_random_jobs(11, 40, nmax=17, lmax=1500))
 
 
-@pytest.mark.parametrize("defer", ["0", "1000"])
-def test_very_long_rows(defer, monkeypatch):
+@pytest.mark.parametrize("defer,rows", [("0", "0"), ("1000", "0"), ("8000", "4")])
+def test_very_long_rows(defer, rows, monkeypatch):
     """Alignments of thousands of columns with hundreds of low-similarity
     regions (the LDS region reduction and its block minima) and some rows
     unrelated from part-way."""
     monkeypatch.setenv("NPGX_ALIGN_DEFER", defer)
+    monkeypatch.setenv("NPGX_ALIGN_DEFER_ROWS", rows)
     rng = np.random.default_rng(21)
     jobs = []
     for _ in range(12):

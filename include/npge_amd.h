@@ -221,6 +221,10 @@ void npgx_aligner_free(npgx_aligner* a);
  *   "RemoveNonStem"      RemoveNonStem --exact (src/algo/RemoveNonStem.cpp:29-45)
  *   "DummyAligner"       AbstractAligner::align_block with DummyAligner
  *                        (AbstractAligner.cpp:51-69, DummyAligner.cpp:18-26)
+ *   "MetaAligner"/"Align" align_block with aligner-type similar: the blocks
+ *                        alignment_needed selects aligned on the GPU, then
+ *                        refine_alignment (AbstractAligner.cpp:51-69,145-177,
+ *                        refine_alignment.cpp:15-190)
  *   "FragmentsExtender"  FragmentsExtender (src/algo/FragmentsExtender.cpp:87-119)
  *   "FixEnds"            FixEnds (src/algo/FixEnds.cpp:117-144)
  *   "ExtendLoopFast"     Pipe ExtendLoopFast (src/algo/lua_lib.lua:697-709,

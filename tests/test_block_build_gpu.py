@@ -137,3 +137,33 @@ def test_remove_non_stem_fixture(case, opts):
     got = canon([[(s, mn, mx, o) for (s, mn, mx, o, _) in b] for b in eng.blocks()])
     want = canon([[(idx[f.seq.name], f.min_pos, f.max_pos, f.ori) for f in b.fragments] for b in exp.blocks])
     assert got == want
+
+
+@pytest.mark.parametrize("cfg", ["tiny", "small"])
+def test_meta_aligner(cfg):
+    """MetaAligner / Align (align_block with the similar aligner + refine_alignment)
+    on unaligned blocks of unequal fragments: the anchors widened by random
+    amounts per fragment, single fragments, and already aligned blocks (left
+    as they are)."""
+    import numpy as np
+    names, seqs = synth.genome_set(cfg)
+    b0 = _stem_blocks(seqs, names)
+    rng = np.random.default_rng(3)
+    blocks = []
+    for b in b0[:400]:
+        nb = []
+        for s, mn, mx, ori, _ in b:
+            a = int(rng.integers(0, 40))
+            z = int(rng.integers(0, 40))
+            nb.append((s, max(0, mn - a), min(len(seqs[s]) - 1, mx + z), ori, None))
+        blocks.append(nb)
+    blocks += [[b[0][:4] + (None,)] for b in b0[400:420]]  # single fragments
+    blocks += b0[420:440]                                   # aligned already
+    ss, eng = _engine(seqs, names)
+    o = orc.BlockSetOracle(seqs, names)
+    eng.set_blocks(blocks).apply("Align")
+    o.set_blocks(blocks)
+    o.apply("MetaAligner")
+    got = eng.blocks()
+    assert got == o.blocks()
+    assert any("-" in (f[4] or "") for b in got for f in b)

@@ -1267,6 +1267,44 @@ static int fix_ends(const std::vector<BSeq>& seqs, const BBlock& b, int min_frag
 }
 
 // ---------------------------------------------------------------- Filter
+// ---------------------------------------------------------------- Rest
+// Rest::run_impl (Rest.cpp:43-72) with add_f (:31-41): per sequence, the
+// fragments sorted (VectorFc::prepare, Fragment::operator<: min, then max),
+// a one-fragment block for the stretch before the first, between consecutive
+// ones and after the last (a sequence without fragments: all of it)
+static void rest(const std::vector<BSeq>& seqs, std::vector<BBlock>& blocks) {
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> fr(seqs.size());
+    for (const BBlock& b : blocks)
+        for (const BFrag& f : b.f) fr[(size_t)f.seq].push_back({f.min, f.max});
+    std::vector<BBlock> add;
+    auto add_f = [&](int s, int64_t mn, int64_t mx) {
+        mn = std::max<int64_t>(0, mn);
+        mx = std::min<int64_t>((int64_t)seqs[(size_t)s].data.size() - 1, mx);
+        if (mn > mx) return;
+        BBlock b;
+        BFrag f;
+        f.seq = s;
+        f.min = mn;
+        f.max = mx;
+        f.ori = 1;
+        b.f.push_back(f);
+        add.push_back(b);
+    };
+    for (size_t s = 0; s < seqs.size(); s++) {
+        auto& ff = fr[s];
+        const int64_t size = (int64_t)seqs[s].data.size();
+        if (ff.empty()) {
+            add_f((int)s, 0, size - 1);
+            continue;
+        }
+        std::sort(ff.begin(), ff.end());
+        add_f((int)s, 0, ff[0].first - 1);
+        for (size_t i = 1; i < ff.size(); i++) add_f((int)s, ff[i - 1].second + 1, ff[i].first - 1);
+        add_f((int)s, ff.back().second + 1, size - 1);
+    }
+    for (auto& b : add) blocks.push_back(b);
+}
+
 // ---------------------------------------------------------------- ConSeq / DeConSeq
 // A gapped row as the reference's AlignmentRow sees it: column -> fragment
 // position (-1 = gap) and back (AlignmentRow.hpp:40-120).
@@ -2112,7 +2150,7 @@ void orc_bs_set_blocks(orc_bs* h, int64_t nb, const int64_t* block_start, const 
 
 // op: 0 FragmentsExtender, 1 FixEnds, 2 Filter, 3 ExtendLoopFast, 4 DummyAligner,
 // 5 RemoveNonStem --exact, 6 DraftPangenome (AnchorFinder on all sequences first),
-// 7 MetaAligner(similar) align_block
+// 7 MetaAligner(similar) align_block, 8 Filter::find_good_subblocks, 9 Rest
 int orc_bs_apply(orc_bs* h, int op) {
     const std::vector<orc::BSeq>& seqs = h->seqs;
     orc::PipelineOpts& o = h->po;
@@ -2156,6 +2194,9 @@ int orc_bs_apply(orc_bs* h, int op) {
             return 0;
         case 7:
             for (auto& b : h->bs.blocks) orc::align_block(seqs, b, 0, o.im);
+            return 0;
+        case 9:
+            orc::rest(seqs, h->bs.blocks);
             return 0;
         case 8:  // Filter::find_good_subblocks only
             for (auto& b : h->bs.blocks) orc::filter_subblocks(seqs, b, o.filter, out);

@@ -252,7 +252,8 @@ PIPELINE_DEFAULTS = dict(
 _PKEYS = list(PIPELINE_DEFAULTS)
 
 OPS = {"FragmentsExtender": 0, "FixEnds": 1, "Filter": 2, "ExtendLoopFast": 3, "DummyAligner": 4,
-       "RemoveNonStem": 5, "DraftPangenome": 6, "MetaAligner": 7, "FindGoodSubblocks": 8}
+       "RemoveNonStem": 5, "DraftPangenome": 6, "MetaAligner": 7, "FindGoodSubblocks": 8,
+       "Rest": 9}
 
 
 def _bs_lib():

@@ -1,0 +1,69 @@
+"""Rest and AnchorLoopFast (lua_lib.lua:741-756) on the engine vs the same
+pipe over the oracle's processors: anchors found on the consensus sequences
+of the DraftPangenome blocks, grown on the consensuses and mapped back by
+DeConSeq; fragments and rows bit-exact."""
+import pytest
+
+from oracle import oracle as orc
+from npge_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def canon(blocks):
+    return sorted(tuple(sorted(b)) for b in blocks)
+
+
+def _engine(seqs, names, blocks=None):
+    from npge_amd import _capi
+    from npge_amd.blockset import BlockSetEngine
+    eng = BlockSetEngine(_capi.SeqSet(seqs, names))
+    if blocks is not None:
+        eng.set_blocks(blocks)
+    return eng
+
+
+def test_rest_kats():
+    """src/test/rest.cpp through the engine."""
+    seqs, names = ["tGGtccgagcgGAcggcc", "tGGtccgagcggacggcc"], ["s1", "s2"]
+    from npge_amd.io import to_atgcn
+    seqs = [to_atgcn(s) for s in seqs]
+    blocks = [[(0, 1, 2, 1, None), (1, 1, 2, 1, None)], [(0, 11, 12, 1, None)]]
+    eng = _engine(seqs, names, blocks).apply("Rest")
+    o = orc.BlockSetOracle(seqs, names)
+    o.set_blocks(blocks)
+    o.apply("Rest")
+    assert eng.blocks() == o.blocks()
+    assert len(eng.blocks()) == 7
+    assert _engine(["AAA"], ["s"], []).apply("Rest").blocks() == [[(0, 0, 2, 1, None)]]
+
+
+def _oracle_loop(o):
+    from npge_amd.anchor_loop import anchor_blocks, block_order
+    o.apply("Filter")
+    o.apply("Rest")
+    o.set_blocks(sorted(o.blocks(), key=block_order))
+    cs = o.conseq()
+    oc = orc.BlockSetOracle(cs, [""] * len(cs))
+    oc.set_blocks(anchor_blocks(orc.AnchorFinder().run(cs, [""] * len(cs))))
+    for op in ("DummyAligner", "FragmentsExtender", "MetaAligner", "ExtendLoopFast"):
+        oc.apply(op)
+    o.deconseq(oc)
+    o.apply("MetaAligner")
+
+
+@pytest.mark.parametrize("cfg", ["tiny", "small"])
+def test_anchor_loop_fast(cfg):
+    from npge_amd.anchor_finder import AnchorFinder
+    from npge_amd.anchor_loop import anchor_loop_fast
+    names, seqs = synth.genome_set(cfg)
+    o = orc.BlockSetOracle(seqs, names)
+    o.apply("DraftPangenome")
+    start = o.blocks()
+    eng = _engine(seqs, names, start)
+    st = anchor_loop_fast(eng, AnchorFinder())
+    o.set_blocks(start)
+    _oracle_loop(o)
+    assert st["consensus_sequences"] > len(start)
+    assert st["anchors"] > 0 and st["mapped_blocks"] > 0
+    assert canon(eng.blocks()) == canon(o.blocks())

@@ -916,7 +916,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (lane == 0) atomicMax(a.slot_epoch, epoch);
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_jobs(SaArgs a) {
+#ifndef SA_WAVES_PER_EU
+#define SA_WAVES_PER_EU 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER_EU))) void k_align_jobs(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
     SlotEnv e = slot_env(a, lds_u64);
@@ -1418,7 +1421,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         put(al->d_order.p, todo.data(), todo.size() * 4);
         NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
         // per-slot scratch: word table, append_aligned stack, regions
-        const size_t slots = (size_t)std::max(1, std::min(nj, 4096));  // 16 waves on each of 256 CUs
+        // SA_WAVES_PER_EU waves on each of the 4 SIMDs of the 256 CUs
+        const size_t slots = (size_t)std::max(1, std::min(nj, 256 * 4 * SA_WAVES_PER_EU));
         uint32_t tlog = 10;
         while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
         const size_t tcap = (size_t)1 << tlog;
@@ -1526,7 +1530,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // budget shrinks as more workgroups must be resident per CU.
         int64_t max_rows = 0;
         for (int32_t j : todo) max_rows = std::max<int64_t>(max_rows, jsum[j]);
-        const int64_t per_cu = std::min<int64_t>(16, std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
+        const int64_t per_cu = std::min<int64_t>(4 * SA_WAVES_PER_EU, std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
         const int64_t budget = LDS_PER_CU / per_cu;
         // word history of the row-parallel search (HIST_SHIFTS x 64 words) when
         // the budget allows

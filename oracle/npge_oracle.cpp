@@ -2245,6 +2245,15 @@ void orc_bs_copy(const orc_bs* h, int64_t* block_start, int32_t* seq, int64_t* m
 
 uint64_t orc_bs_hash(const orc_bs* h) { return orc::blockset_hash(h->bs); }
 
+// goodColumns (goodColumns.cpp:177-209) of nrows rows of `length` chars each
+int orc_good_columns(int nrows, const char* rows, int length, int min_identity, int min_length, int32_t* out) {
+    Strings r((size_t)nrows);
+    for (int i = 0; i < nrows; i++) r[(size_t)i].assign(rows + (size_t)i * (size_t)length, (size_t)length);
+    const std::vector<int> s = orc::goodColumns(r, length, min_identity, min_length);
+    for (int i = 0; i < length; i++) out[i] = s[(size_t)i];
+    return 0;
+}
+
 // ConSeq: the text of the sequence each block becomes (in block order), two
 // calls: total size (out == NULL), then the bytes and n_blocks + 1 offsets
 int64_t orc_bs_conseq(const orc_bs* h, char* out, int64_t* off) {

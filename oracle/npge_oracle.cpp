@@ -21,6 +21,7 @@
 //     and s[p > size] is a per-row sentinel that equals nothing (counted in
 //     g_past_end_reads so tests can see whether an input exercised it).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -29,6 +30,7 @@
 #include <tuple>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 typedef uint64_t hash_t;
@@ -262,6 +264,28 @@ struct AnchorResult {
     int64_t n_found_frags = 0; // before truncation
 };
 
+// BlocksJobs (BlocksJobs.cpp:38-240) over `workers` threads: fn(i, tid) for every
+// block index i, blocks claimed `chunk` at a time from a shared counter.  Callers
+// write per-index results, so the output does not depend on the thread count.
+template <class F>
+static void for_blocks(size_t n, int workers, F fn, size_t chunk = 16) {
+    if (workers <= 1 || n < 2) {
+        for (size_t i = 0; i < n; i++) fn(i, 0);
+        return;
+    }
+    std::atomic<size_t> next(0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::min<int>(workers, (int)((n + chunk - 1) / chunk)); t++)
+        pool.emplace_back([&, t] {
+            for (;;) {
+                size_t a = next.fetch_add(chunk);
+                if (a >= n) break;
+                for (size_t i = a; i < std::min(n, a + chunk); i++) fn(i, t);
+            }
+        });
+    for (auto& th : pool) th.join();
+}
+
 struct AnchorFinder {
     int anchor = 20;
     int64_t fp_x1e4 = 1000;     // Decimal("0.1")
@@ -270,6 +294,7 @@ struct AnchorFinder {
     uint32_t seed = 1;
     std::vector<hash_t> explicit_params;  // overrides seed when non-empty
     std::vector<hash_t> used_hashes;      // AnchorFinder.cpp:30-35 (persistent)
+    int workers = 1;                      // FragmentTG threads of pass 2 (one sequence per task)
 
     // AnchorFinder.cpp:393-406
     int run(std::vector<Seq>& all, AnchorResult& out) {
@@ -351,8 +376,9 @@ struct AnchorFinder {
         out.n_collected = (int64_t)hashes.size();
 
         // pass 2: FragmentTask AnchorFinder.cpp:283-326
-        std::vector<FoundFragment> ffs;
-        for (size_t r = 0; r < seqs.size(); r++) {
+        std::vector<std::vector<FoundFragment>> per_seq(seqs.size());
+        for_blocks(seqs.size(), workers, [&](size_t r, int) {
+            std::vector<FoundFragment>& ffs = per_seq[r];
             const std::string& s = seqs[r]->data;
             const int k = anchor;
             int ns = 0;
@@ -381,7 +407,9 @@ struct AnchorFinder {
                 rev = reuse_hash(rev, k, complement_char(rm), complement_char(ad), false);
                 test_and_push();
             }
-        }
+        }, 1);
+        std::vector<FoundFragment> ffs;
+        for (auto& v : per_seq) ffs.insert(ffs.end(), v.begin(), v.end());
         out.n_found_frags = (int64_t)ffs.size();
         // fragmenttg_postprocess AnchorFinder.cpp:356-391
         std::sort(ffs.begin(), ffs.end());
@@ -1738,7 +1766,9 @@ struct PipelineOpts {
     int max_iterations = 10;
     FilterOpts filter;
     bool do_filter = true;
+    int workers = 1;  // BlocksJobs workers (the reference's --workers); 1 = reference-exact sequential run
 };
+
 
 // RemoveNonStem --exact (RemoveNonStem.cpp:29-45)
 static void remove_non_stem(BlockSetO& bs, bool exact) {
@@ -1852,18 +1882,20 @@ static void extend_loop_fast(BlockSetO& bs, const PipelineOpts& o, PipelineStats
         std::sort(mu_hashes.begin(), mu_hashes.end());
         mu_hashes.erase(std::unique(mu_hashes.begin(), mu_hashes.end()), mu_hashes.end());
         // ExtendAndFix: FragmentsExtender --extend-length-portion:=0.5, FixEnds
-        for (BBlock& b : work)
-            fragments_extender(seqs, b, o.extend_length, o.portion_x1e4, o.im, &st.aligned_residues);
+        std::vector<int64_t> aligned((size_t)std::max(o.workers, 1), 0);
+        std::vector<BBlock> outs(work.size());
+        std::vector<int> res(work.size(), 0);
+        for_blocks(work.size(), o.workers, [&](size_t i, int t) {
+            BBlock& b = work[i];
+            fragments_extender(seqs, b, o.extend_length, o.portion_x1e4, o.im, &aligned[(size_t)t]);
+            if (b.f.empty() || !b.f[0].has_row) return;  // FixEnds asserts alignment; anchors have rows
+            res[i] = fix_ends(seqs, b, o.fix_min_fragment, o.fix_min_identity_x1e4, outs[i]);
+        });
+        for (int64_t a : aligned) st.aligned_residues += a;
         std::vector<BBlock> fixed;
-        for (BBlock& b : work) {
-            if (b.f.empty() || !b.f[0].has_row) {  // FixEnds asserts alignment; anchors have rows
-                fixed.push_back(std::move(b));
-                continue;
-            }
-            BBlock out;
-            int r = fix_ends(seqs, b, o.fix_min_fragment, o.fix_min_identity_x1e4, out);
-            if (r == 0) fixed.push_back(std::move(b));
-            else if (r == 1) fixed.push_back(std::move(out));
+        for (size_t i = 0; i < work.size(); i++) {
+            if (res[i] == 0) fixed.push_back(std::move(work[i]));
+            else if (res[i] == 1) fixed.push_back(std::move(outs[i]));
         }
         // Move target=target other=unchanged
         for (BBlock& b : unchanged) fixed.push_back(std::move(b));
@@ -1917,16 +1949,19 @@ static void draft_pangenome(std::vector<BSeq>& seqs, AnchorFinder& af, const Pip
     st.anchor_blocks = (int64_t)bs.blocks.size();
     remove_non_stem(bs, true);
     st.stem_blocks = (int64_t)bs.blocks.size();
-    for (BBlock& b : bs.blocks) align_block(seqs, b, 1, o.im);  // DummyAligner
+    for_blocks(bs.blocks.size(), o.workers,
+               [&](size_t i, int) { align_block(seqs, bs.blocks[i], 1, o.im); });  // DummyAligner
     extend_loop_fast(bs, o, st);
     if (o.do_filter) {
+        std::vector<std::vector<BBlock>> subs(bs.blocks.size());
+        std::vector<int> res(bs.blocks.size());
+        for_blocks(bs.blocks.size(), o.workers,
+                   [&](size_t i, int) { res[i] = filter_block(seqs, bs.blocks[i], o.filter, subs[i]); });
         std::vector<BBlock> out;
-        for (BBlock& b : bs.blocks) {
-            std::vector<BBlock> sub;
-            int r = filter_block(seqs, b, o.filter, sub);
-            if (r == 0) out.push_back(std::move(b));
-            else if (r == 1)
-                for (auto& x : sub) out.push_back(std::move(x));
+        for (size_t i = 0; i < bs.blocks.size(); i++) {
+            if (res[i] == 0) out.push_back(std::move(bs.blocks[i]));
+            else if (res[i] == 1)
+                for (auto& x : subs[i]) out.push_back(std::move(x));
         }
         bs.blocks.swap(out);
     }
@@ -2147,6 +2182,11 @@ void orc_bs_set_blocks(orc_bs* h, int64_t nb, const int64_t* block_start, const 
         h->bs.blocks.push_back(blk);
     }
 }
+
+// Worker count for DraftPangenome: BlocksJobs for the per-block stages, FragmentTG
+// (one sequence per task) for AnchorFinder's pass 2; the Bloom pass stays
+// sequential (racy in the reference when threaded); results identical for every count
+void orc_bs_set_workers(orc_bs* h, int workers) { h->af.workers = h->po.workers = workers < 1 ? 1 : workers; }
 
 // op: 0 FragmentsExtender, 1 FixEnds, 2 Filter, 3 ExtendLoopFast, 4 DummyAligner,
 // 5 RemoveNonStem --exact, 6 DraftPangenome (AnchorFinder on all sequences first),

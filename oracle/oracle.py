@@ -266,6 +266,7 @@ def _bs_lib():
         L.orc_bs_set_blocks.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orc_bs_apply.argtypes = [vp, ctypes.c_int]
         L.orc_bs_apply.restype = ctypes.c_int
+        L.orc_bs_set_workers.argtypes = [vp, ctypes.c_int]
         L.orc_bs_counts.argtypes = [vp, vp]
         L.orc_bs_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orc_bs_hash.argtypes = [vp]
@@ -318,6 +319,12 @@ class BlockSetOracle:
         data = "".join(rows).encode() or b"\0"
         _bs_lib().orc_bs_set_blocks(self._h, len(blocks), _ptr(bs), _ptr(seq), _ptr(mn), _ptr(mx),
                                     _ptr(ori), _ptr(ro), _ptr(rl), data)
+
+    def set_workers(self, workers):
+        """BlocksJobs worker threads for DraftPangenome / ExtendLoopFast's
+        per-block stages (BlocksJobs.cpp:38-240); output identical for any count."""
+        _bs_lib().orc_bs_set_workers(self._h, int(workers))
+        return self
 
     def apply(self, op):
         rc = _bs_lib().orc_bs_apply(self._h, OPS[op])

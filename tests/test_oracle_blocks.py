@@ -144,3 +144,17 @@ def test_draft_pangenome_runs(cfg):
             if ori == -1:
                 text = text[::-1].translate(str.maketrans("ATGC", "TACG"))
             assert row.replace("-", "") == text
+
+
+def test_oracle_workers_identical():
+    """The threaded oracle (FragmentTG per sequence in AnchorFinder pass 2,
+    BlocksJobs per block, BlocksJobs.cpp:38-240) gives the same blocks as the
+    1-worker run: bench.py's cpu_baseline "all_cores" leg times the same work."""
+    from npge_amd import synth
+    names, seqs = synth.genome_set("tiny")
+    ref = orc.BlockSetOracle(seqs, names).apply("DraftPangenome")
+    for w in (2, 5):
+        o = orc.BlockSetOracle(seqs, names).set_workers(w).apply("DraftPangenome")
+        assert o.hash() == ref.hash()
+        assert o.blocks() == ref.blocks()
+        assert o.stats() == ref.stats()

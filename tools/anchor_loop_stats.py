@@ -9,7 +9,7 @@ from npge_amd.anchor_finder import AnchorFinder
 from npge_amd.anchor_loop import anchor_loop_fast
 import time
 _capi.check(_capi.lib().npgx_set_device(0))
-for cfg in ("tiny", "small", "C2"):
+for cfg in (sys.argv[1:] or ["tiny", "small", "C2"]):
     names, seqs = synth.genome_set(cfg)
     ss = _capi.SeqSet(seqs, names)
     eng = BlockSetEngine(ss)

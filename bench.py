@@ -32,12 +32,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2")
+    ap.add_argument("--config", default="C3",
+                    help="synthetic genome set (npge_amd/synth.py); C3 = the 17-genome ≥50x target config")
     ap.add_argument("--mode", choices=("replicas", "sharded"), default="replicas")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", default="C2", help="synthetic config timed for cpu_baseline")
+    ap.add_argument("--cpu-sample", default=None, help="synthetic config timed for cpu_baseline (default: --config)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU runs (median) after one warm-up")
     return ap.parse_args()
 
 
@@ -101,9 +103,27 @@ def main():
     if roofline is not None:
         roofline.update(pmc_traffic(dom["name"], args.config))
 
+    # the boundary takes host buffers: time the upload (to_atgcn + H2D + pack,
+    # npgx_seqset_create) on its own; `value` excludes it (inputs resident in
+    # HBM), `pcie_inclusive` adds it to every step
+    import statistics
+    import time
+    ups = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        ss2 = _capi.SeqSet(seqs, names)
+        torch.cuda.synchronize()
+        ups.append(time.perf_counter() - t)
+        ss2.close()
+    up = statistics.median(ups)
+    step_s = dt / args.steps
+    pcie = {"upload_ms": round(up * 1e3, 3),
+            "value": round(harness.throughput(bp, 1 if sharded else world, 1, step_s + up) / 1e6, 3)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_sample)
+        cpu = cpu_baseline(args.cpu_sample or args.config, args.cpu_runs)
 
     if rank == 0:
         line = {
@@ -122,11 +142,13 @@ def main():
             "config": {"workload": job.workload_name(args.config), "bp_per_rank": bp,
                        "genomes": synth.CONFIGS[args.config][0], "anchor_size": 20,
                        "anchor_fp": 0.1, "max_anchor_fragments": 100000,
+                       "inputs": "resident in HBM before the timed region (upload: pcie_inclusive)",
                        "parallelism": ("sharded x%d (RCCL)" % world) if sharded
                        else "replica-per-gpu x%d" % world},
             "last_step": info,
             "kernels_last_step": kernels,
             "roofline": roofline,
+            "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -151,40 +173,82 @@ def pmc_traffic(kernel, config):
     return {"traffic": None}
 
 
-def cpu_baseline(config):
-    """The CPU restatement (oracle/) timed on this host on the same workload:
-    single thread (reference 1-worker semantics) and, under "all_cores", with
-    FragmentTG + BlocksJobs threading over the host cores this job may use (the
-    reference's --workers; the Bloom pass sequential)."""
+def _cpu_info():
+    """Host CPU facts for the record: nproc (the whole machine), the cores this
+    job may use, and the lscpu model name."""
+    import subprocess
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = os.cpu_count()
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                info["model"] = ln.split(":", 1)[1].strip()
+    except Exception:  # lscpu missing: leave the model out
+        pass
+    return info
+
+
+def cpu_baseline(config, runs=5):
+    """The CPU restatement (oracle/) timed on this host on the same workload,
+    built -O3 -march=native on this host (oracle/Makefile `native`): one thread
+    (reference 1-worker semantics) and, under "all_cores", with FragmentTG +
+    BlocksJobs threading (the reference's --workers; the Bloom pass sequential)
+    over every core this job is allotted.  Each is the median of `runs` timed
+    runs after one warm-up (steady clock), input packing excluded like the GPU
+    side's upload."""
+    import statistics
     import time
     from npge_amd import synth
     from oracle import oracle as orc
+    native = orc.use_native()
     names, seqs = synth.genome_set(config)
     bp = synth.total_bp(seqs)
 
     def run(workers):
-        t = time.perf_counter()
         o = orc.BlockSetOracle(seqs, names, seed=1)
         o.set_workers(workers)
+        t = time.perf_counter()
         o.apply("DraftPangenome")
-        return time.perf_counter() - t, o.hash()
+        dt = time.perf_counter() - t
+        print("cpu_baseline: %s workers=%d %.3f s" % (config, workers, dt), file=sys.stderr, flush=True)
+        return dt, o.hash()
 
-    t1, h1 = run(1)
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    workers = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)), 16))
-    tn, hn = run(workers)
+    def median_of(workers):
+        run(workers)  # warm-up
+        ts, hs = [], set()
+        for _ in range(runs):
+            dt, h = run(workers)
+            ts.append(dt)
+            hs.add(h)
+        if len(hs) != 1:
+            raise AssertionError("oracle DraftPangenome not reproducible across runs")
+        return statistics.median(ts), hs.pop(), ts
+
+    info = _cpu_info()
+    # the cores this job is allotted: the scheduler's OMP_NUM_THREADS share when
+    # set (the GPU box's per-GPU CPU share), else every core in the affinity mask
+    workers = max(1, int(os.environ.get("OMP_NUM_THREADS", info["affinity"])))
+    workers = min(workers, info["affinity"])
+    t1, h1, ts1 = median_of(1)
+    tn, hn, tsn = median_of(workers)
     if hn != h1:
         raise AssertionError("threaded oracle DraftPangenome differs from the 1-thread run")
     return {"value": round(bp / 1e6 / t1, 4), "unit": "Mbp/s", "cores": 1, "kind": "port",
-            "sample": "%s synthetic set (%d bp), one full step of the same workload, oracle/ "
-                      "C++ -O3, 1 thread" % (config, bp), "seconds": round(t1, 3),
+            "sample": "%s synthetic set (%d bp), one full DraftPangenome step of the same workload, "
+                      "oracle/ C++ %s, 1 thread, median of %d runs after 1 warm-up"
+                      % (config, bp, "-O3 -march=native" if native else "-O3 (prebuilt)", runs),
+            "seconds": round(t1, 3), "runs_s": [round(x, 3) for x in ts1],
+            "host": info,
             "all_cores": {"value": round(bp / 1e6 / tn, 4), "cores": workers, "seconds": round(tn, 3),
-                          "threading": "FragmentTG per sequence (AnchorFinder pass 2), BlocksJobs per block (DummyAligner, FragmentsExtender, "
-                                       "FixEnds, Filter); the Bloom pass and the loop's set "
-                                       "operations sequential"}}
+                          "runs_s": [round(x, 3) for x in tsn],
+                          "threading": "FragmentTG per sequence (AnchorFinder pass 2), BlocksJobs per block "
+                                       "(DummyAligner, FragmentsExtender, FixEnds, Filter); the Bloom pass "
+                                       "and the loop's set operations sequential"}}
+
 
 if __name__ == "__main__":
     main()

@@ -25,13 +25,46 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+def use_native():
+    """Selects a copy of the restatement built -O3 -march=native on THIS host
+    (bench.py's cpu_baseline leg, timed on the GPU box's own cores).  The build
+    goes to the temp directory under a name keyed by the sources and the host's
+    CPU flags, so a library built on another machine is never picked up.  Must
+    be called before the first lib().  Returns False (prebuilt library kept)
+    when no compiler is available."""
+    global _LIB_PATH
+    import hashlib
+    import tempfile
+    if _lib is not None:
+        return _LIB_PATH.endswith("_native.so")
+    srcs = ["npge_oracle.cpp", "general_aligner.cpp"]
+    h = hashlib.sha1()
+    for f in srcs + ["log_score.inc"]:
+        h.update(open(os.path.join(_HERE, f), "rb").read())
+    try:
+        h.update(open("/proc/cpuinfo", "rb").read().split(b"\n\n")[0])
+    except OSError:
+        pass
+    out = os.path.join(tempfile.gettempdir(), "npgx_oracle_%s_native.so" % h.hexdigest()[:16])
+    if not os.path.exists(out):
+        tmp = out + ".%d.tmp" % os.getpid()
+        try:
+            subprocess.check_call(["g++", "-O3", "-march=native", "-std=c++17", "-fPIC", "-shared",
+                                   "-pthread", "-o", tmp] + [os.path.join(_HERE, f) for f in srcs])
+        except (OSError, subprocess.CalledProcessError):
+            return False
+        os.replace(tmp, out)
+    _LIB_PATH = out
+    return True
+
+
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or any(
+        if _LIB_PATH.endswith("liboracle.so") and (not os.path.exists(_LIB_PATH) or any(
             os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, f))
             for f in ("npge_oracle.cpp", "general_aligner.cpp")
-        ):
+        )):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         u64, i64, i32, u32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32

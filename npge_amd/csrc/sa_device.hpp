@@ -485,6 +485,16 @@ struct Proc {
     uint32_t epoch;   // global word-table epoch (carried from one Proc to the next)
     uint32_t lepoch;  // LDS word-table epoch
     int n_aligned_calls, n_shifts, n_gaps, n_fast;
+    // Segment of a split job (similar_aligner.hip, "Long jobs"): the top-level
+    // walk stops when its state (every row's pos) equals one of the sync
+    // states tg[t*n + row], t in [tm, tK) -- process_cols is memoryless in
+    // pos, so the walk from that state on is the next segment's.
+    const int* tg;
+    int tK, tm;      // targets, the next one tested (wave-uniform)
+    int tv;          // this row's position in target tm (relative to the view)
+    int tbase;       // this row's view start in the full row (targets are full-row positions)
+    bool chk;        // the top-level frame is running: test the targets
+    bool stop;       // a target was reached (pos == target tm)
 #ifdef NPGX_SA_PROFILE
     // fast_run, equal/mismatch steps, try_gap, try_aligned, vector words,
     // vector compares, chunks, calls, append_end, child return (reverse)
@@ -494,7 +504,36 @@ struct Proc {
     __device__ __forceinline__ Proc(const WaveCtx& w_, const Params& P_, const Slot& S_, char* ob_, int cap_,
                                     uint32_t ep, uint32_t lep)
         : w(w_), P(P_), S(S_), ob(ob_), cap(cap_), pos(0), col(0), ovf(false), epoch(ep), lepoch(lep),
-          n_aligned_calls(0), n_shifts(0), n_gaps(0), n_fast(0) {}
+          n_aligned_calls(0), n_shifts(0), n_gaps(0), n_fast(0), tg(nullptr), tK(0), tm(0), tv(0), tbase(0),
+          chk(false), stop(false) {}
+
+    // targets t in [t0, tK) of a segment (row-major, n per target; positions
+    // in the full rows, the view of this row starting at `base`)
+    __device__ __forceinline__ void set_targets(const int* targets, int t0, int nt, int base) {
+        tg = targets;
+        tm = t0;
+        tK = nt;
+        tbase = base;
+        tv = (tm < tK && w.act) ? tg[tm * w.n + w.lane] - tbase : 0;
+    }
+
+    // Every row advances by c columns from pos (states pos, pos+1, .., pos+c):
+    // the d with pos + d == target tm, or -1.  A target some row has passed
+    // can no longer be reached (pos only grows): the next one is tested.
+    __device__ __forceinline__ int target_hit(int c) {
+        while (tm < tK) {
+            const int d = w.act ? tv - pos : 0;
+            if (any_lane(w, d < 0)) {
+                tm++;
+                if (tm < tK && w.act) tv = tg[tm * w.n + w.lane] - tbase;
+                continue;
+            }
+            const int d0 = __builtin_amdgcn_readlane(d, 0);
+            if (d0 <= c && all_eq(w, d)) return d0;
+            return -1;
+        }
+        return -1;
+    }
 
     __device__ __forceinline__ void put(int c, char x) {
         if (c < cap) ob[(size_t)w.lane * cap + c] = x;
@@ -507,6 +546,15 @@ struct Proc {
     __device__ __forceinline__ void append_cols(int cols) {
         if (w.act)
             for (int j = 0; j < cols; j++) put(col + j, (char)ch(pos + j));
+        if (chk) {
+            const int d = target_hit(cols);
+            if (d >= 0) {  // the columns past the target are not kept
+                pos += w.act ? d : 0;
+                col += d;
+                stop = true;
+                return;
+            }
+        }
         pos += w.act ? cols : 0;
         col += cols;
     }
@@ -538,7 +586,7 @@ struct Proc {
 
     // Columns mode: consume the columns process_cols takes with is_equal /
     // try_mismatch.  Returns 0: the next column needs a rows-mode step,
-    // 1: a row ended (is_stop(0) -> append_all).
+    // 1: a row ended (is_stop(0) -> append_all), 2: a segment target reached.
     __device__ __forceinline__ int fast_run() {
         __syncthreads();
         while (true) {
@@ -593,6 +641,16 @@ struct Proc {
                     break;
                 }
                 break;  // the mismatch window crosses the chunk: restart the chunk at k
+            }
+            if (chk) {  // (the consumed columns advance every row by one)
+                const int d = target_hit(k);
+                if (d >= 0) {
+                    pos += w.act ? d : 0;
+                    col += d;
+                    stop = true;
+                    __syncthreads();
+                    return 2;
+                }
             }
             pos += w.act ? k : 0;
             col += k;
@@ -912,11 +970,13 @@ struct Proc {
 
     // One step of process_cols (SimilarAligner.cpp:351-368): a columns-mode run,
     // then one rows-mode step.  Returns 0 = keep stepping, 1 = frame finished,
-    // 2 = descend into a child (sh = this row's shift).
+    // 2 = descend into a child (sh = this row's shift); a segment target
+    // reached (stop) shows as 0 or 1.
     __device__ __forceinline__ int step(int& sh) {
         SA_T0(t0);
         const int fr = fast_run();
         SA_ACC(0, t0);
+        if (fr == 2) return 1;
         if (fr == 1) {
             append_all();  // is_stop(0)
             return 1;
@@ -965,6 +1025,8 @@ struct Proc {
         col = col0;
         int depth = 0;
         bool fresh = true;
+        stop = false;
+        chk = tm < tK;
         while (true) {
             int r;
             if (fresh && any_lane(w, v.len == 0)) {  // process_cols :345-350
@@ -973,7 +1035,9 @@ struct Proc {
             } else {
                 int sh = 0;
                 r = step(sh);
+                if (stop) return col - col0;  // (depth 0: only the top-level frame tests targets)
                 if (r == 2) {
+                    chk = false;
                     if (depth >= S.st_depth_max) {  // excluded by the host's sizing
                         ovf = true;
                         return col - col0;
@@ -1014,8 +1078,10 @@ struct Proc {
                 cm_reverse(w, ob, cap, c0, col);
             }
             pos += w.act ? child_len : 0;
+            chk = depth == 0 && tm < tK;
             append_cols(P.ac);
             SA_ACC(9, t5);
+            if (stop) return col - col0;
         }
     }
 };

@@ -52,6 +52,25 @@ struct SaSub {
     int64_t out_off;    // byte offset in the sub-job output pool (n rows x out_cap)
 };
 
+// Long jobs are split into segments at sync states (see "Long jobs" at
+// k_split_find): segment k runs process_seqs from state k to the first later
+// state its walk passes through exactly.
+struct SaSplit {
+    int32_t job;
+    int32_t K;          // segments (K - 1 sync states)
+    int64_t tgt;        // first int of its sync states (K - 1 states x n rows)
+    int32_t seg0;       // its first segment task
+    int32_t win;        // half-width of the sync word search window
+};
+
+struct SaSeg {
+    int32_t split;      // index into splits
+    int32_t k;          // segment index
+    int32_t cap;        // output columns
+    int32_t pad;
+    int64_t out;        // byte offset of its n x cap output rows in seg_pool
+};
+
 struct SaArgs {
     const char* rows;
     const int64_t* row_off;
@@ -98,6 +117,14 @@ struct SaArgs {
     int64_t pool_cap;
     int64_t max_sub;
     int32_t* fin;              // the deferred jobs
+    // split long jobs (order[] entries < 0 are segment tasks -(t+1))
+    const SaSplit* splits;
+    const SaSeg* segs;
+    int32_t* targets;          // sync states (k_split_find)
+    int4* seg_res;             // per segment: next segment (K: ran to the end, -1: idle), columns, overflow
+    int64_t* seg_wall;         // per segment: wall clock at start and end (job statistics)
+    unsigned int* seg_done;    // per split job: segments finished
+    unsigned char* seg_pool;
 };
 
 // number of columns c in [c0, c1) identical over all rows (score_of :416-426)
@@ -338,37 +365,28 @@ typedef __attribute__((address_space(3))) int LdsInt;
 // minimum).  The survivors go to `out` in order with .w = the number of
 // identical columns in the region (score_of before re-alignment); returns
 // their count, or -1 when the LDS area is too small.
-__device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, int wf, int min_length,
-                              char* area_g, int area_bytes, int4* out) {
-    typedef __attribute__((address_space(3))) unsigned long long LdsU64w;
-    const int lane = w.lane;
-    const int nw = (L + 63) >> 6;
-    if ((long long)nw * 16 > area_bytes) return -1;
-    LdsU64w* gm = (LdsU64w*)area_g;  // identical-column bits
-    LdsU64w* sm = gm + nw;           // region-start bits
-    for (int b = 0; b < nw; b += 4) {
-        bool eq[4];
-        char x[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int c = (b + u) * 64 + lane;
-            eq[u] = c < L;
-            x[u] = eq[u] ? A[c] : 0;
-        }
-        for (int r = 1; r < w.n; r++) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int c = (b + u) * 64 + lane;
-                eq[u] &= (c < L ? A[(size_t)r * cap + c] : 0) == x[u];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const unsigned long long m = ballot(eq[u]);
-            if (lane == 0 && b + u < nw) gm[b + u] = m;
-        }
+typedef __attribute__((address_space(3))) unsigned long long LdsU64w;
+
+template <bool WG>
+__device__ __forceinline__ void wave_or_wg_sync() {
+    if (WG) {
+        __syncthreads();
+    } else {  // one wave's LDS accesses in program order across its lanes
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+}
+
+// make_regions + reduce_regions from the identical-column bits gm[0, nw) in
+// LDS, the arrays after them (area_bytes in all, gm included); WG: the
+// workgroup is this one wave (barriers), else a wave of a larger workgroup
+// working alone (wave-level ordering of its LDS accesses)
+template <bool WG>
+__device__ int regions_from_bits(const WaveCtx& w, LdsU64w* gm, int nw, int L, int wf, int min_length,
+                                 int area_bytes, int4* out) {
+    const int lane = w.lane;
+    LdsU64w* sm = gm + nw;  // region-start bits
     int R0 = 0;
     for (int q = lane; q < nw; q += 64) {
         const unsigned long long g = gm[q];
@@ -379,7 +397,7 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
         R0 += __popcll(st);
     }
     R0 = wave_sum(R0);
-    __syncthreads();
+    wave_or_wg_sync<WG>();
     // per region 12 bytes: start (-1: merged away), weight | good << 31, and
     // next | prev << 16 (0xFFFF: none); a region ends where the next alive starts
     const long long need = (long long)nw * 16 + (long long)R0 * 12;
@@ -407,14 +425,14 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
         }
         k += bcast(pre, 63);
     }
-    __syncthreads();
+    wave_or_wg_sync<WG>();
     for (int i = lane; i < R0; i += 64) {
         const int len = (i + 1 < R0 ? rx[i + 1] : L) - rx[i];
         const int good = (int)((unsigned)rw[i] >> 31);
         rw[i] = (good << 31) | (good ? len : len * wf);  // Region::set_weight :48-54
         lk[i] = (i + 1 < R0 ? i + 1 : 0xFFFF) | ((i > 0 ? i - 1 : 0xFFFF) << 16);
     }
-    __syncthreads();
+    wave_or_wg_sync<WG>();
     const int WM = 0x7fffffff;
     int R = R0;
     // one merge of the minimum region mi with its alive neighbours (merge_region :94-119)
@@ -427,7 +445,7 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
         const int z = ((unsigned)rw[mi] >> 31) ? 0 : 1;
         const int after = hq ? lk[q] & 0xFFFF : q;
         const int keep_prev = (lk[keep] >> 16) & 0xFFFF;
-        __syncthreads();
+        wave_or_wg_sync<WG>();
         if (lane == 0) {
             if (hp) rx[mi] = -1;
             if (hq) rx[q] = -1;
@@ -435,7 +453,7 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
             lk[keep] = after | (keep_prev << 16);
             if (after != 0xFFFF) lk[after] = (lk[after] & 0xFFFF) | (keep << 16);
         }
-        __syncthreads();
+        wave_or_wg_sync<WG>();
         hp_out = hp;
         hq_out = hq;
         p_out = p;
@@ -529,8 +547,41 @@ __device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, i
         if (alive) out[k + __popcll(m & ((1ull << lane) - 1ull))] = rg;
         k += __popcll(m);
     }
-    __syncthreads();
+    wave_or_wg_sync<WG>();
     return R;
+}
+
+
+__device__ int regions_in_lds(const WaveCtx& w, const char* A, int cap, int L, int wf, int min_length,
+                              char* area_g, int area_bytes, int4* out) {
+    const int lane = w.lane;
+    const int nw = (L + 63) >> 6;
+    if ((long long)nw * 16 > area_bytes) return -1;
+    LdsU64w* gm = (LdsU64w*)area_g;  // identical-column bits
+    for (int b = 0; b < nw; b += 4) {
+        bool eq[4];
+        char x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = (b + u) * 64 + lane;
+            eq[u] = c < L;
+            x[u] = eq[u] ? A[c] : 0;
+        }
+        for (int r = 1; r < w.n; r++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int c = (b + u) * 64 + lane;
+                eq[u] &= (c < L ? A[(size_t)r * cap + c] : 0) == x[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned long long m = ballot(eq[u]);
+            if (lane == 0 && b + u < nw) gm[b + u] = m;
+        }
+    }
+    __syncthreads();
+    return regions_from_bits<true>(w, gm, nw, L, wf, min_length, area_bytes, out);
 }
 
 // AbstractAligner.cpp:89-102: drop columns that are '-' in every row
@@ -775,7 +826,8 @@ __device__ __forceinline__ bool tail_identical(const WaveCtx& w, const char* B, 
     return true;
 }
 
-// realing_end (:461-484) on B + AbstractAligner remove_gaps; returns the length
+// realing_end (:461-484) on B; returns the length (remove_gaps has nothing to
+// remove from the similar aligner's columns, see k_align_jobs)
 __device__ int finish_tail(Proc& pr, const WaveCtx& w, char* B, char* C, int cap, int L, char* stage,
                            int stage_bytes, int ac, bool& ovf) {
     pr.ob = B;
@@ -791,8 +843,18 @@ __device__ int finish_tail(Proc& pr, const WaveCtx& w, char* B, char* C, int cap
         }
     }
     __syncthreads();
-    if (!ovf) L = remove_pure_gap_cols(w, B, cap, L);
     return L;
+}
+
+// Width of region ri of a deferred job in B: a good region or a bad one whose
+// re-alignment did not gain keeps its columns of A, else the re-alignment's
+// columns; -1: the re-alignment overflowed
+__device__ __forceinline__ int fin_width(const SaArgs& a, int4 rg) {
+    const int len = rg.y - rg.x + 1;
+    if (rg.z > 0) return len;
+    const int2 res = a.sub_res[-rg.z - 1];
+    if (res.x < 0) return -1;
+    return res.y > rg.w ? res.x : len;  // more identical columns: the re-alignment (score_of :445-455)
 }
 
 // k_align_sub: every bad region of every deferred job, one wave each
@@ -836,8 +898,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (lane == 0) atomicMax(a.slot_epoch, epoch);
 }
 
-// k_align_finish: the deferred jobs' B = good regions of A + the better of
-// each bad region and its re-alignment, then realing_end and remove_gaps
+// k_align_finish: realing_end on the deferred jobs' B (= good regions of A +
+// the better of each bad region and its re-alignment, k_fin_copy)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_finish(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
@@ -862,47 +924,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         char* C = B + (size_t)n * cap;
         const int R = a.job_nreg[j];
         const int4* jr = a.job_regions + job.reg_off;
-        int colB = 0;
-        bool ovf = false;
-        for (int ri = 0; ri < R && !ovf; ri++) {
-            const int4 rg = jr[ri];
-            const int len = rg.y - rg.x + 1;
-            if (rg.z > 0) {
-                if (colB + len > cap) {
-                    ovf = true;
-                    break;
-                }
-                cm_copy(w, A, B, cap, rg.x, colB, len);
-                colB += len;
-                continue;
-            }
-            const int sub = -rg.z - 1;
-            const int2 res = a.sub_res[sub];
-            if (res.x < 0) {
-                ovf = true;
-                break;
-            }
-            if (res.y > rg.w) {  // the re-alignment has more identical columns: keep it (reversed back)
-                if (colB + res.x > cap) {
-                    ovf = true;
-                    break;
-                }
-                const SaSub d = a.subs[sub];
-                const char* out = (const char*)(a.pool + d.out_off + 256);
-                for (int r = 0; r < n; r++)
-                    for (int c = lane; c < res.x; c += 64)
-                        B[(size_t)r * cap + colB + c] = out[(size_t)r * d.out_cap + res.x - 1 - c];
-                __syncthreads();
-                colB += res.x;
-            } else {
-                if (colB + len > cap) {
-                    ovf = true;
-                    break;
-                }
-                cm_copy(w, A, B, cap, rg.x, colB, len);
-                colB += len;
-            }
+        // B was assembled by k_fin_copy: its length, or an overflow
+        int colB = 0, bad = 0;
+        for (int ri = lane; ri < R; ri += 64) {
+            const int wd = fin_width(a, jr[ri]);
+            bad |= wd < 0;
+            colB += max(wd, 0);
         }
+        colB = wave_sum(colB);
+        bool ovf = ballot(bad) != 0 || colB > cap;
         Proc pr(w, a.P, e.S, B, cap, epoch, lepoch);
         const int L = finish_tail(pr, w, B, C, cap, colB, e.stage, a.stage_bytes, a.P.ac, ovf);
         if (lane == 0) {
@@ -914,6 +944,628 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         __syncthreads();
     }
     if (lane == 0) atomicMax(a.slot_epoch, epoch);
+}
+
+// ------------------------------------------------------------------ Long jobs
+// A wave walks a job's columns one dependent step after another, so a launch
+// lasts as long as its longest job (C3: 46 jobs of up to 20k columns and 17
+// rows, 14 ms on one wave).  process_cols (SimilarAligner.cpp:344-369) is
+// memoryless in the row cursors: every decision reads the rows forward from
+// pos (is_equal, try_mismatch, try_gap, try_aligned's min_tail, append_end's
+// row ends), so the walk from a state (pos_0 .. pos_n-1) -- and its output
+// columns -- is process_seqs of the row suffixes from that state.  A long job
+// is therefore cut at K-1 sync states chosen where the rows surely align (the
+// middle of a 32-mer that occurs exactly once in a window of every row around
+// the same fraction of the rows), and segment k runs process_seqs of the
+// suffixes from state k until its top-level walk is exactly at a later state
+// m (then the walk from there is segment m's) or ends.  The job's alignment is
+// the chain 0 -> m1 -> m2 .. -> end of the segments' columns: bit-exact by
+// construction whether or not the speculation holds (a segment whose walk
+// passes a state without landing on it just continues to the next one).
+// Only uniform advances of the top-level frame are tested (fast_run chunks and
+// append_cols); a state inside a multi-column step is still exact because the
+// rest of such a step is identical columns (try_mismatch's mc columns,
+// apply_gap's gc, the aligned word after a child), which process_cols from
+// the state appends one by one.
+static constexpr int SPLIT_W = 12;       // sync word length (the reference's aligned_check is 10)
+static constexpr int SPLIT_C = 128;      // candidate words per sync state (two per lane)
+static constexpr int SPLIT_RMAX = 512;   // largest search half-width
+static constexpr int SPLIT_SPAN = 2 * SPLIT_RMAX + SPLIT_C + 1;  // word positions per row window
+static constexpr int SPLIT_HT = 2048;    // LDS hash table entries (> 1.75 x SPLIT_SPAN)
+static constexpr int SPLIT_KMAX = 128;   // segments per job at most
+static constexpr size_t SPLIT_LDS = (size_t)SPLIT_HT * 12 + (size_t)64 * SPLIT_C * 2 + SPLIT_SPAN + SPLIT_W + 80;
+
+__device__ __forceinline__ uint32_t base2(uint32_t c) {  // A C G T -> 0..3, anything else 4
+    return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
+}
+
+// Sync state t of split job s (the start of segment t+1), one wave each
+// (tasks[b] = (s, t)).  Candidates: row 0's 12-mers at x0 .. x0+127, x0 the
+// fraction (t+1)/K of row 0.  Row by row, every 12-mer of the row's window
+// around the same fraction goes into an LDS hash table (tagged with the row,
+// first and last position per word) and each candidate looks itself up: it
+// survives when it occurs exactly once in every row's window.  The state is
+// the middle of the longest run of surviving consecutive candidates, W/2 into
+// its word -- inside an identical stretch of at least 12 columns, which the
+// walk crosses column by column when it is in step there.  None survives: -1
+// in every row (segment t+1 idles).
+__global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, int n_tasks) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
+    uint32_t* hkey = lds_w;                        // tag << 24 | word
+    uint32_t* hlo = hkey + SPLIT_HT;               // max of tag << 16 | (0xFFFF - first position)
+    uint32_t* hhi = hlo + SPLIT_HT;                // max of tag << 16 | last position
+    uint16_t* P = (uint16_t*)(hhi + SPLIT_HT);     // [row][candidate] window offset of its occurrence
+    unsigned char* ch = (unsigned char*)(P + 64 * SPLIT_C);
+    const int b = blockIdx.x;
+    if (b >= n_tasks) return;
+    const int lane = threadIdx.x;
+    const int2 tk = tasks[b];
+    const SaSplit sp = a.splits[tk.x];
+    const SaJob job = a.jobs[sp.job];
+    const int n = job.n, t = tk.y, R = min(sp.win, SPLIT_RMAX);
+    const int span = 2 * R + SPLIT_C + 1;
+    for (int e = lane; e < SPLIT_HT; e += 64) {
+        hkey[e] = 0u;
+        hlo[e] = 0u;
+        hhi[e] = 0u;
+    }
+    const uint32_t WM = (1u << (2 * SPLIT_W)) - 1u;
+    uint32_t cw[2] = {0u, 0u};
+    bool ok[2] = {false, false};
+    // window chars of row i, loaded one row ahead into registers
+    constexpr int PER = (SPLIT_SPAN + SPLIT_W + 63) / 64;
+    unsigned char nx[PER];
+    int lo_next = 0;
+    {
+        const int li = a.row_len[job.row0];
+        const char* ri = a.rows + a.row_off[job.row0];
+        lo_next = (int)((int64_t)li * (t + 1) / sp.K) - R;
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int q = u * 64 + lane, p = lo_next + q;
+            nx[u] = (q < span + SPLIT_W - 1 && p >= 0 && p < li) ? (unsigned char)ri[p] : 0;
+        }
+    }
+    for (int i = 0; i < n; i++) {
+        const int lo = lo_next;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PER; u++) ch[u * 64 + lane] = nx[u];
+        __syncthreads();
+        if (i + 1 < n) {
+            const int li = a.row_len[job.row0 + i + 1];
+            const char* ri = a.rows + a.row_off[job.row0 + i + 1];
+            lo_next = (int)((int64_t)li * (t + 1) / sp.K) - R;
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int q = u * 64 + lane, p = lo_next + q;
+                nx[u] = (q < span + SPLIT_W - 1 && p >= 0 && p < li) ? (unsigned char)ri[p] : 0;
+            }
+        }
+        const uint32_t tag = (uint32_t)i + 1u;
+        if (i == 0) {  // the candidates: row 0 at window offsets R + c
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int q = R + lane + 64 * h;
+                uint32_t x = 0, bad = 0;
+                for (int j = 0; j < SPLIT_W; j++) {
+                    const uint32_t c = base2(ch[q + j]);
+                    bad |= c >> 2;
+                    x = (x << 2) | (c & 3u);
+                }
+                cw[h] = x & WM;
+                ok[h] = bad == 0 && lo >= 0;
+            }
+        }
+        // every word of the window into the table
+        for (int q = lane; q < span; q += 64) {
+            uint32_t x = 0, bad = 0;
+            for (int j = 0; j < SPLIT_W; j++) {
+                const uint32_t c = base2(ch[q + j]);
+                bad |= c >> 2;
+                x = (x << 2) | (c & 3u);
+            }
+            if (bad) continue;
+            x &= WM;
+            const uint32_t key = (tag << 24) | x;
+            uint32_t e = (x * 2654435761u) >> (32 - 11);
+            while (true) {
+                const uint32_t k = hkey[e];
+                if (k == key) break;
+                if ((k >> 24) != tag) {  // empty for this row (stale): claim
+                    const uint32_t old = atomicCAS(&hkey[e], k, key);
+                    if (old == k || old == key) break;
+                    continue;
+                }
+                e = (e + 1) & (SPLIT_HT - 1);
+            }
+            atomicMax(&hlo[e], (tag << 16) | (0xFFFFu - (uint32_t)q));
+            atomicMax(&hhi[e], (tag << 16) | (uint32_t)q);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (!ok[h]) continue;
+            const uint32_t key = (tag << 24) | cw[h];
+            uint32_t e = (cw[h] * 2654435761u) >> (32 - 11);
+            int at = -1;
+            while (true) {
+                const uint32_t k = hkey[e];
+                if (k == key) {
+                    const uint32_t f = hlo[e], l = hhi[e];
+                    if ((f >> 16) == tag && (l >> 16) == tag && 0xFFFFu - (f & 0xFFFFu) == (l & 0xFFFFu))
+                        at = (int)(l & 0xFFFFu);
+                    break;
+                }
+                if ((k >> 24) != tag) break;
+                e = (e + 1) & (SPLIT_HT - 1);
+            }
+            ok[h] = at >= 0;
+            if (at >= 0) P[i * SPLIT_C + lane + 64 * h] = (uint16_t)at;
+        }
+    }
+    // the longest run of surviving consecutive candidates, its middle
+    const unsigned long long m0 = ballot(ok[0]), m1 = ballot(ok[1]);
+    int best = -1, blen = 0, run = 0;
+    for (int c = 0; c < SPLIT_C; c++) {  // (wave-uniform scan of the two masks)
+        const bool o = c < 64 ? ((m0 >> c) & 1ull) : ((m1 >> (c - 64)) & 1ull);
+        run = o ? run + 1 : 0;
+        if (run > blen) {
+            blen = run;
+            best = c - (run - 1) / 2;
+        }
+    }
+    __syncthreads();
+    int* out = a.targets + sp.tgt + (int64_t)t * n;
+    if (lane < n) {
+        int v = -1;
+        if (best >= 0) {
+            const int li = a.row_len[job.row0 + lane];
+            const int lo = (int)((int64_t)li * (t + 1) / sp.K) - R;
+            v = lo + (int)P[lane * SPLIT_C + best] + SPLIT_W / 2;
+        }
+        out[lane] = v;
+    }
+}
+
+// ---------------------------------------------------- split jobs after their segments
+static constexpr int POST_THREADS = 256;
+static constexpr int FIN_PARTS = 16;  // workgroups assembling one deferred job's B
+static constexpr size_t POST_LDS = 144 * 1024;
+
+__device__ __forceinline__ long long wave_sum64(long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (long long)shfl64((unsigned long long)v, threadIdx.x % 64 ^ o);
+    return v;
+}
+
+// filter_reverse for a wave of a larger workgroup (no workgroup barrier):
+// row r's segment [s0, s1) gap-filtered and reversed to C + r*cstride;
+// returns this lane's row length
+__device__ int filter_reverse_wave(const WaveCtx& w, const char* src, int cap, char* C, int cstride, int s0,
+                                   int s1) {
+    int my_len = 0;
+    for (int r = 0; r < w.n; r++) {
+        const char* a = src + (size_t)r * cap;
+        char* c = C + (size_t)r * cstride;
+        int k = 0;
+        for (int base = s1 - 1; base >= s0; base -= 64) {
+            const int idx = base - w.lane;
+            const bool in = idx >= s0;
+            const char x = in ? a[idx] : '-';
+            const bool keep = in && x != '-';
+            const unsigned long long m = ballot(keep);
+            if (keep) c[k + __popcll(m & ((1ull << w.lane) - 1ull))] = x;
+            k += __popcll(m);
+        }
+        if (w.lane == r) my_len = k;
+    }
+    return my_len;
+}
+
+// exclusive prefix sum over the POST_THREADS threads of the workgroup (every
+// thread calls it); *total = the sum of all
+__device__ __forceinline__ int block_scan_excl(int v, int* total, int* scratch4) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) scratch4[wid] = inc;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int q = 0; q < POST_THREADS / 64; q++) {
+        const int s = scratch4[q];
+        before += q < wid ? s : 0;
+        all += s;
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - v;
+}
+
+// FindLowSimilar::make_regions (:62-80) + reduce_regions (:121-130) by the
+// whole workgroup, from the identical-column bits gm[0, nw): the reference
+// merges the first minimum-weight region with its neighbours until every
+// weight reaches min_length.  A region whose (weight, index) is below that of
+// every region within two places is merged by the reference before anything
+// touches its neighbours (merged weights only grow, and nothing within two
+// places can become the minimum first), and two such regions are at least
+// three places apart: so every round merges all of them at once, with the
+// reference's result.  Survivors to out[] as (start, stop, good, identical
+// columns); returns their count, or -1 when the LDS area is too small or
+// more than out_cap survive.
+__device__ int regions_block(LdsU64w* gm, int nw, int L, int wf, int min_length, int area_bytes, int4* out,
+                             int out_cap, int* scratch4) {
+    const int tid = threadIdx.x;
+    // region starts: where the identical bit flips (and column 0)
+    int cnt = 0;
+    for (int q = tid; q < nw; q += POST_THREADS) {
+        const unsigned long long g = gm[q];
+        const unsigned long long valid = (q < nw - 1 || (L & 63) == 0) ? ~0ull : ((1ull << (L & 63)) - 1);
+        unsigned long long st = (g ^ ((g << 1) | (q > 0 ? (gm[q - 1] >> 63) : (g & 1ull)))) & valid;
+        if (q == 0) st |= 1ull;
+        cnt += __popcll(st);
+    }
+    int R = 0;
+    block_scan_excl(cnt, &R, scratch4);
+    const long long need = (long long)nw * 8 + (long long)R * 9 + 64;
+    if (need > area_bytes) return -1;
+    LdsInt* rx = (LdsInt*)(gm + nw);
+    LdsInt* rw = rx + R;  // weight | good << 31
+    unsigned char* mf = (unsigned char*)(rw + R);  // this round's merging regions
+    // starts in order: words dealt out in contiguous runs per thread
+    {
+        const int per = (nw + POST_THREADS - 1) / POST_THREADS;
+        const int q0 = min(nw, tid * per), q1 = min(nw, q0 + per);
+        int c = 0;
+        for (int q = q0; q < q1; q++) {
+            const unsigned long long g = gm[q];
+            const unsigned long long valid = (q < nw - 1 || (L & 63) == 0) ? ~0ull : ((1ull << (L & 63)) - 1);
+            unsigned long long st = (g ^ ((g << 1) | (q > 0 ? (gm[q - 1] >> 63) : (g & 1ull)))) & valid;
+            if (q == 0) st |= 1ull;
+            c += __popcll(st);
+        }
+        int tot = 0;
+        int i = block_scan_excl(c, &tot, scratch4);
+        for (int q = q0; q < q1; q++) {
+            const unsigned long long g = gm[q];
+            const unsigned long long valid = (q < nw - 1 || (L & 63) == 0) ? ~0ull : ((1ull << (L & 63)) - 1);
+            unsigned long long st = (g ^ ((g << 1) | (q > 0 ? (gm[q - 1] >> 63) : (g & 1ull)))) & valid;
+            if (q == 0) st |= 1ull;
+            for (; st; st &= st - 1) {
+                const int col = q * 64 + __ffsll((long long)st) - 1;
+                rx[i] = col;
+                rw[i] = (int)((g >> (col & 63)) & 1ull) << 31;
+                i++;
+            }
+        }
+    }
+    __syncthreads();
+    const int WM = 0x7fffffff;
+    for (int i = tid; i < R; i += POST_THREADS) {  // Region::set_weight :48-54
+        const int len = (i + 1 < R ? rx[i + 1] : L) - rx[i];
+        const int good = (int)((unsigned)rw[i] >> 31);
+        rw[i] = (good << 31) | (good ? len : len * wf);
+    }
+    __syncthreads();
+    __shared__ int s_any;
+    while (R >= 2) {
+        if (tid == 0) s_any = 0;
+        __syncthreads();
+        int any = 0;
+        for (int i = tid; i < R; i += POST_THREADS) {
+            const int wi = rw[i] & WM;
+            bool m = wi < min_length;
+            for (int d = -2; d <= 2 && m; d++) {
+                const int k = i + d;
+                if (d == 0 || k < 0 || k >= R) continue;
+                const int wk = rw[k] & WM;
+                m = wi < wk || (wi == wk && i < k);
+            }
+            mf[i] = m;
+            any |= m;
+        }
+        if (any) s_any = 1;
+        __syncthreads();
+        if (!s_any) break;
+        // merge (merge_region :94-119) and compact, tile by tile in order
+        int dest = 0;
+        for (int t0 = 0; t0 < R; t0 += POST_THREADS) {
+            const int i = t0 + tid;
+            int keep = 0, nx = 0, nwt = 0;
+            if (i < R) {
+                const bool m = mf[i];
+                const bool rem = (i > 0 && mf[i - 1]) || (i + 1 < R && mf[i + 1]);
+                keep = !rem;
+                nx = rx[i];
+                nwt = rw[i];
+                if (m) {
+                    int wsum = nwt & WM;
+                    if (i > 0) {
+                        nx = rx[i - 1];
+                        wsum += rw[i - 1] & WM;
+                    }
+                    if (i + 1 < R) wsum += rw[i + 1] & WM;
+                    nwt = ((((unsigned)nwt >> 31) ? 0 : 1) << 31) | wsum;
+                }
+            }
+            int kt = 0;
+            const int at = dest + block_scan_excl(keep, &kt, scratch4);
+            if (keep) {
+                rx[at] = nx;
+                rw[at] = nwt;
+            }
+            __syncthreads();
+            dest += kt;
+        }
+        R = dest;
+        __syncthreads();
+    }
+    if (R > out_cap) return -1;
+    // survivors with their identical columns (score_of before re-alignment)
+    for (int i = tid; i < R; i += POST_THREADS) {
+        const int x = rx[i], y = (i + 1 < R ? rx[i + 1] : L) - 1;
+        const int good = (int)((unsigned)rw[i] >> 31);
+        int c = 0;
+        if (!good)
+            for (int q = x >> 6; q <= (y >> 6); q++) {
+                const int lo = q == (x >> 6) ? (x & 63) : 0, hi = q == (y >> 6) ? (y & 63) : 63;
+                c += __popcll(gm[q] & ((hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & (~0ull << lo)));
+            }
+        out[i] = make_int4(x, y, good, c);
+    }
+    __syncthreads();
+    return R;
+}
+
+// One workgroup per split job, after k_align_jobs: the chain of its segments
+// (0 -> m1 -> m2 .. -> end) copied into the job's A with the identical-column
+// bits (count_equal_cols :416-426) on the way, FindLowSimilar's regions from
+// those bits (wave 0, in LDS: make_regions + reduce_regions), and
+// fix_bad_regions deferred: every bad region gap-filtered and reversed into C
+// and queued for k_align_sub; k_fin_copy / k_align_finish assemble B and run
+// realing_end.  A chain that overflowed or does not fit marks the job for the
+// whole-job re-run (status 1).
+__global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_p[];
+    __shared__ int pk[SPLIT_KMAX], pcols[SPLIT_KMAX], pdst[SPLIT_KMAX];
+    __shared__ int s_np, s_L0, s_fail, s_R, s_scan[POST_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const SaSplit sp = a.splits[blockIdx.x];
+    const int j = sp.job;
+    const SaJob job = a.jobs[j];
+    const int n = job.n, cap = job.cap;
+    char* A = (char*)(a.scratch + job.scratch);
+    char* C = A + 2 * (size_t)n * cap;
+    WaveCtx w;
+    w.lane = lane;
+    w.n = n;
+    w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    w.act = lane < n;
+    if (tid == 0) {
+        int k = 0, col = 0, np = 0, fail = 0;
+        while (k < sp.K) {
+            const int4 r = a.seg_res[sp.seg0 + k];
+            if (r.x <= k || r.z || col + r.y > cap) {  // (an idle segment is never on the chain)
+                fail = 1;
+                break;
+            }
+            pk[np] = sp.seg0 + k;
+            pcols[np] = r.y;
+            pdst[np] = col;
+            np++;
+            col += r.y;
+            k = r.x;
+        }
+        s_np = np;
+        s_L0 = col;
+        s_fail = fail;
+    }
+    __syncthreads();
+    const int L0 = s_L0, nw = (L0 + 63) >> 6;
+    if (s_fail || (long long)nw * 16 > lds_bytes) {
+        if (tid == 0) {
+            a.job_len[j] = 0;
+            a.job_status[j] = 1;
+        }
+        return;
+    }
+    LdsU64w* gm = (LdsU64w*)lds_p;
+    for (int q = tid; q < nw; q += POST_THREADS) gm[q] = 0ull;
+    __syncthreads();
+    for (int p = 0; p < s_np; p++) {  // four columns per thread, rows read as dwords
+        const SaSeg g = a.segs[pk[p]];
+        const char* src = (const char*)(a.seg_pool + g.out);
+        const int cols = pcols[p], d0 = pdst[p];
+        for (int c = 4 * tid; c < cols; c += 4 * POST_THREADS) {
+            const int nb = min(4, cols - c);
+            const uint32_t x0 = *(const uint32_t*)(src + c);  // (rows of 16-aligned length: in bounds)
+            uint32_t diff = 0;
+            char* d = A + d0 + c;
+            for (int b = 0; b < nb; b++) d[b] = (char)(x0 >> (8 * b));
+            for (int r = 1; r < n; r++) {
+                const uint32_t x = *(const uint32_t*)(src + (size_t)r * g.cap + c);
+                diff |= x ^ x0;
+                char* dr = A + (size_t)r * cap + d0 + c;
+                for (int b = 0; b < nb; b++) dr[b] = (char)(x >> (8 * b));
+            }
+            for (int b = 0; b < nb; b++)
+                if (!((diff >> (8 * b)) & 0xFFu)) {
+                    const int col = d0 + c + b;
+                    atomicOr((unsigned long long*)&gm[col >> 6], 1ull << (col & 63));
+                }
+        }
+    }
+    __syncthreads();
+    int4* jr = a.job_regions + job.reg_off;
+    const int R = regions_block(gm, nw, L0, a.P.wf, a.P.min_length, lds_bytes, jr, job.reg_cap, s_scan);
+    if (R < 0 || R > job.reg_cap) {
+        if (tid == 0) {
+            a.job_len[j] = 0;
+            a.job_status[j] = 1;
+        }
+        return;
+    }
+    // every bad region a sub-job: pool bytes and sub-job ids in region order
+    if (wid == 0) {
+        long long need = 0;
+        int nbad = 0;
+        for (int ri = lane; ri < R; ri += 64) {
+            const int4 rg = jr[ri];
+            if (!rg.z) {
+                nbad++;
+                need += sub_bytes(n, sub_out_cap(cap, rg.y - rg.x + 1));
+            }
+        }
+        nbad = wave_sum(nbad);
+        need = wave_sum64(need);
+        long long base = 0, s0 = 0;
+        if (lane == 0 && nbad) {
+            base = reserve(&a.alloc[0], (unsigned long long)need, (unsigned long long)a.pool_cap);
+            if (base >= 0) s0 = (long long)atomicAdd(&a.alloc[1], (unsigned long long)nbad);
+        }
+        base = (long long)bcast64((unsigned long long)base, 0);
+        s0 = (long long)bcast64((unsigned long long)s0, 0);
+        if (base < 0) {
+            if (lane == 0) s_R = -1;
+        } else {
+            long long off = base;
+            int sub = (int)s0;
+            for (int c0 = 0; c0 < R; c0 += 64) {
+                const int ri = c0 + lane;
+                const int4 rg = ri < R ? jr[ri] : make_int4(0, 0, 1, 0);
+                const bool bad = ri < R && !rg.z;
+                const int oc = bad ? sub_out_cap(cap, rg.y - rg.x + 1) : 0;
+                const long long by = bad ? sub_bytes(n, oc) : 0;
+                long long pb = by;  // inclusive scans over the chunk
+                int pc = bad ? 1 : 0;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const long long tb = (long long)shfl64((unsigned long long)pb, max(lane - o, 0));
+                    const int tc = __shfl(pc, max(lane - o, 0));
+                    if (lane >= o) {
+                        pb += tb;
+                        pc += tc;
+                    }
+                }
+                if (bad) {
+                    const int sn = sub + pc - 1;
+                    SaSub d;
+                    d.job = j;
+                    d.x = rg.x;
+                    d.out_cap = oc;
+                    d.pad = 0;
+                    d.out_off = off + pb - by;
+                    a.subs[sn] = d;
+                    jr[ri] = make_int4(rg.x, rg.y, -(sn + 1), rg.w);
+                }
+                off += (long long)shfl64((unsigned long long)pb, 63);
+                sub += __shfl(pc, 63);
+            }
+        }
+    }
+    __syncthreads();
+    if (s_R < 0) {  // sub-job pool full
+        if (tid == 0) {
+            a.job_len[j] = 0;
+            a.job_status[j] = 1;
+        }
+        return;
+    }
+    for (int ri = wid; ri < R; ri += POST_THREADS / 64) {
+        const int4 rg = jr[ri];
+        if (rg.z > 0) continue;
+        const SaSub d = a.subs[-rg.z - 1];
+        const int len = filter_reverse_wave(w, A, cap, C + rg.x, cap, rg.x, rg.y + 1);
+        if (w.act) ((int*)(a.pool + d.out_off))[lane] = len;
+    }
+    if (tid == 0) {
+        a.job_nreg[j] = R;
+        a.fin[atomicAdd(&a.counters[1], 1u)] = j;
+        a.job_len[j] = L0;
+        a.job_status[j] = 3;
+    }
+}
+
+// k_fin_copy: B of every deferred job, FIN_PARTS workgroups per job, each a
+// range of B's columns; column c of B comes from the region whose output
+// offsets hold it (binary search over the offsets in LDS)
+__global__ __launch_bounds__(POST_THREADS) void k_fin_copy(SaArgs a, int lds_ints, int* g_dst) {
+    extern __shared__ __attribute__((aligned(16))) int dst_l[];
+    __shared__ int s_tot;
+    const int fn = blockIdx.x / FIN_PARTS, part = blockIdx.x % FIN_PARTS;
+    if (fn >= (int)a.counters[1]) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int j = a.fin[fn];
+    const SaJob job = a.jobs[j];
+    const int n = job.n, cap = job.cap;
+    const char* A = (const char*)(a.scratch + job.scratch);
+    char* B = (char*)A + (size_t)n * cap;
+    const int R = a.job_nreg[j];
+    const int4* jr = a.job_regions + job.reg_off;
+    // output offsets (every part computes them; the global fallback is
+    // written with equal values by every part of the job)
+    int* dst = R + 1 <= lds_ints ? dst_l : g_dst + job.reg_off + j;
+    if (tid < 64) {
+        int carry = 0, bad = 0;
+        if (lane == 0) dst[0] = 0;
+        for (int c0 = 0; c0 < R; c0 += 64) {
+            const int ri = c0 + lane;
+            const int wd = ri < R ? fin_width(a, jr[ri]) : 0;
+            bad |= wd < 0;
+            int pre = max(wd, 0);
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(pre, o);
+                if (lane >= o) pre += t;
+            }
+            if (ri < R) dst[ri + 1] = carry + pre;
+            carry += __shfl(pre, 63);
+        }
+        bad = (int)(ballot(bad) != 0);
+        if (lane == 0) s_tot = (bad || carry > cap) ? -1 : carry;  // k_align_finish marks the overflow
+    }
+    __syncthreads();
+    const int tot = s_tot;
+    if (tot <= 0) return;
+    const int c0 = (int)((int64_t)tot * part / FIN_PARTS), c1 = (int)((int64_t)tot * (part + 1) / FIN_PARTS);
+    for (int c = c0 + tid; c < c1; c += POST_THREADS) {
+        int lo = 0, hi = R - 1;  // the region ri with dst[ri] <= c < dst[ri+1]
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (dst[mid] <= c) lo = mid;
+            else hi = mid - 1;
+        }
+        const int4 rg = jr[lo];
+        const int off = c - dst[lo];
+        bool from_sub = false;
+        const char* sp = A + rg.x + off;
+        size_t stride = (size_t)cap;
+        if (rg.z <= 0) {
+            const int2 res = a.sub_res[-rg.z - 1];
+            if (res.y > rg.w) {  // the re-alignment, reversed back
+                const SaSub d = a.subs[-rg.z - 1];
+                sp = (const char*)(a.pool + d.out_off + 256) + (res.x - 1 - off);
+                stride = (size_t)d.out_cap;
+                from_sub = true;
+            }
+        }
+        (void)from_sub;
+        int r = 0;
+        for (; r + 4 <= n; r += 4) {
+            const char x0 = sp[(size_t)r * stride], x1 = sp[(size_t)(r + 1) * stride];
+            const char x2 = sp[(size_t)(r + 2) * stride], x3 = sp[(size_t)(r + 3) * stride];
+            B[(size_t)r * cap + c] = x0;
+            B[(size_t)(r + 1) * cap + c] = x1;
+            B[(size_t)(r + 2) * cap + c] = x2;
+            B[(size_t)(r + 3) * cap + c] = x3;
+        }
+        for (; r < n; r++) B[(size_t)r * cap + c] = sp[(size_t)r * stride];
+    }
 }
 
 #ifndef SA_WAVES_PER_EU
@@ -933,7 +1585,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         if (lane == 0) jn = atomicAdd(a.next_job, 1u);
         jn = bcast(jn, 0);
         if (jn >= (unsigned)a.n_jobs) break;
-        const int j = a.order[jn];
+        const int oj = a.order[jn];
+        // oj < 0: segment task -oj-1 of a split job -- process_seqs of the row
+        // suffixes from its sync state into its own output; the wave that
+        // finishes the job's last segment goes on with the chained result in A
+        const bool chained = oj < 0;
+        const int seg_t = -oj - 1;
+        SaSeg sg{};
+        SaSplit sp{};
+        if (chained) {
+            sg = a.segs[seg_t];
+            sp = a.splits[sg.split];
+        }
+        const int j = chained ? sp.job : oj;
         const SaJob job = a.jobs[j];
         const int n = job.n;
         if (n == 0) {
@@ -961,12 +1625,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         char* C = B + (size_t)n * cap;
         int sb = a.stage_bytes;  // stage bytes free for segments / region arrays
         bool lds_abc = false;
+        const int* T = chained ? a.targets + sp.tgt : nullptr;  // sync state k >= 1 at T[(k-1)*n + row]
+        const int start = (chained && sg.k > 0 && w.act) ? T[(sg.k - 1) * n + lane] : 0;
+        const bool idle = chained && any_lane(w, start < 0);  // no sync state found
         View v0{nullptr, 0, 1};
         if (w.act) {
-            v0.p = a.rows + a.row_off[job.row0 + lane];
-            v0.len = a.row_len[job.row0 + lane];
+            v0.p = a.rows + a.row_off[job.row0 + lane] + start;
+            v0.len = a.row_len[job.row0 + lane] - start;
         }
-        if (a.aligner_type == 0) {
+        if (a.aligner_type == 0 && !idle) {
             // the rows into LDS when they fit: every char(q) of the greedy walk
             // is then an LDS read instead of a global one
             int off = 0, tot = 0;
@@ -981,7 +1648,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
             // copied to the global A or B at the end
             const int abc = 3 * n * cap;
             const bool may_defer = a.defer != 0 && cap >= a.defer && n >= a.defer_rows;
-            if (!may_defer && ((tot + 15) & ~15) + abc <= a.stage_bytes) {
+            if (!chained && !may_defer && ((tot + 15) & ~15) + abc <= a.stage_bytes) {
                 lds_abc = true;
                 sb = (a.stage_bytes - abc) & ~15;
                 A = stage + sb;
@@ -1010,7 +1677,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
                 if (w.act) v0.p = stage + off;
             }
         }
-        bool ovf = false, deferred = false;
+        bool deferred = false, ovf = false;
         int L = 0;
         if (a.aligner_type == 1) {
             // DummyAligner: pad to the longest row
@@ -1025,10 +1692,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         } else {
             // 1. process_seqs
             // one Proc for every process_seqs call of the job (state is per call)
-            Proc pr(w, a.P, S, A, cap, epoch, lepoch);
+            Proc pr(w, a.P, S, chained ? (char*)(a.seg_pool + sg.out) : A, chained ? sg.cap : cap, epoch, lepoch);
             long long t0 = clock64();
-            const int L0 = pr.run(v0, 0);
-            ovf = any_lane(w, pr.ovf);
+            int L0 = 0;
+            if (!idle) {
+                if (chained) pr.set_targets(T, sg.k, sp.K - 1, start);
+                L0 = pr.run(v0, 0);
+                ovf = any_lane(w, pr.ovf);
+            }
+            if (chained) {  // the segment's result; k_split_post chains the job's segments
+                if (lane == 0) {
+                    a.seg_res[seg_t] = idle ? make_int4(-1, 0, 0, 0)
+                                            : make_int4(pr.stop ? pr.tm + 1 : sp.K, L0, ovf ? 1 : 0, 0);
+                    if (a.job_stats) {
+                        a.seg_wall[2 * seg_t] = (int64_t)w_job;
+                        a.seg_wall[2 * seg_t + 1] = (int64_t)wall_clock64();
+                    }
+                }
+                epoch = pr.epoch;
+                lepoch = pr.lepoch;
+                continue;
+            }
             t_ph[0] = clock64() - t0;
             t0 = clock64();
 
@@ -1148,8 +1832,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
             lepoch = pr.lepoch;
         }
         __syncthreads();
-        // 4. remove pure-gap columns
-        if (!ovf && !deferred) L = remove_pure_gap_cols(w, B, cap, L);
+        // 4. remove pure-gap columns (AbstractAligner::remove_gaps): the
+        // similar aligner's alignments have none -- every column of
+        // process_seqs holds a letter (append_cols, apply_gap's shifted rows,
+        // the longest tail of append_all / append_end), and fix_bad_regions /
+        // realing_end only concatenate such columns -- so only the dummy
+        // aligner (whose input rows may hold gaps) needs the pass
+        if (!ovf && !deferred && a.aligner_type == 1) L = remove_pure_gap_cols(w, B, cap, L);
         if (lds_abc && !ovf) {  // the result to where the host reads it (A for status 2, else B)
             __syncthreads();
             char* dst = gA + (B == A ? 0 : (size_t)n * cap);
@@ -1163,6 +1852,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         }
         if (lane == 0 && a.job_stats) {  // only when the statistics are wanted
             int64_t* js = a.job_stats + (size_t)j * NPGX_JOB_STATS;
+            const int64_t w0 = (int64_t)w_job;
             js[0] = clock64() - t_job;
             js[1] = L;
             js[2] = st_calls;
@@ -1174,7 +1864,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
             js[8] = t_ph[0];
             js[9] = t_ph[1];
             js[10] = t_ph[2];
-            js[11] = (int64_t)w_job;
+            js[11] = w0;
             for (int q = 0; q < 10; q++) js[12 + q] = st_prof[q];
             js[22] = t_regions;
             js[23] = (int64_t)wall_clock64();
@@ -1266,6 +1956,23 @@ struct npgx_aligner {
     DevBuf<unsigned long long> d_alloc;
     DevBuf<unsigned int> d_counters;
     DevBuf<unsigned char> d_pool;
+    // long jobs split into segments (k_split_find, run_segment): jobs of at
+    // least two rows are cut every `split` columns of their longest row
+    // (NPGX_ALIGN_SPLIT; 0: never)
+    int split = 512;
+    std::vector<SaSplit> h_splits;
+    std::vector<SaSeg> h_segs;
+    std::vector<int2> h_ftasks;
+    std::vector<int32_t> h_queue, h_jmax;
+    DevBuf<SaSplit> d_splits;
+    DevBuf<SaSeg> d_segs;
+    DevBuf<int2> d_ftasks;
+    DevBuf<int32_t> d_targets;
+    DevBuf<int4> d_seg_res;
+    DevBuf<int64_t> d_seg_wall;
+    DevBuf<unsigned int> d_seg_done;
+    DevBuf<unsigned char> d_seg_pool;
+    DevBuf<int> d_reg_dst;  // k_fin_copy's region offsets when they do not fit its LDS
     // last result
     std::vector<char> out;
     std::vector<int64_t> out_off;
@@ -1304,6 +2011,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     cost.resize(n_jobs);
     std::vector<int32_t>& jsum = al->h_jsum;  // residues per job
     jsum.resize(n_jobs);
+    std::vector<int32_t>& jmax = al->h_jmax;  // longest row per job
+    jmax.resize(n_jobs);
     int64_t scratch = 0, n_reg = 0, n_sub_max = 0;
     int max_n = 1, max_len = 1, max_cap = 1;
     const int wf = weight_factor(o.min_identity_x1e4);
@@ -1344,6 +2053,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         n_sub_max += (J.reg_cap + 1) / 2;
         cost[j] = double(n) * double(sum);
         jsum[j] = (int32_t)std::min<int64_t>(sum, INT32_MAX);
+        jmax[j] = mx;
         max_n = std::max(max_n, n);
         max_len = std::max(max_len, mx);
         max_cap = std::max<int>(max_cap, J.cap);
@@ -1415,10 +2125,61 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 max_cap = std::max<int>(max_cap, J.cap);
             }
         }
-        const int nj = (int)todo.size();
+        // the work queue: the segments of the split jobs (heaviest first), then
+        // the other jobs
+        std::vector<SaSplit>& splits = al->h_splits;
+        std::vector<SaSeg>& segs = al->h_segs;
+        std::vector<int2>& ftasks = al->h_ftasks;
+        std::vector<int32_t>& queue = al->h_queue;
+        splits.clear();
+        segs.clear();
+        ftasks.clear();
+        queue.clear();
+        int64_t n_tgt = 0, seg_bytes = 0;
+        if (attempt == 0 && o.aligner_type == 0 && al->split > 0) {
+            for (int32_t j : todo) {
+                const SaJob& J = jobs[j];
+                const int mx = jmax[j];
+                const int K = std::min(SPLIT_KMAX, mx / al->split);
+                if (J.n < 2 || K < 2 || mx < 4 * SPLIT_W) continue;
+                SaSplit sp;
+                sp.job = j;
+                sp.K = K;
+                sp.tgt = n_tgt;
+                sp.seg0 = (int32_t)segs.size();
+                sp.win = std::min(SPLIT_RMAX, 64 + mx / 64);
+                n_tgt += (int64_t)(K - 1) * J.n;
+                for (int k = 0; k < K; k++) {
+                    SaSeg g;
+                    g.split = (int32_t)splits.size();
+                    g.k = k;
+                    // room for the whole suffix (a walk that passes its states
+                    // without landing on one runs to the end)
+                    const int64_t rest = mx - (int64_t)mx * k / K + sp.win;
+                    g.cap = (int32_t)std::min<int64_t>(J.cap, (2 * rest + 64 + 15) & ~15ll);
+                    g.pad = 0;
+                    g.out = seg_bytes;
+                    seg_bytes += ((int64_t)J.n * g.cap + 255) & ~255ll;
+                    queue.push_back(-(int32_t)segs.size() - 1);
+                    segs.push_back(g);
+                }
+                for (int t = 0; t + 1 < K; t++) ftasks.push_back(make_int2((int)splits.size(), t));
+                splits.push_back(sp);
+            }
+        }
+        if (splits.empty()) {
+            queue = todo;
+        } else {
+            std::vector<uint8_t> is_split(n_jobs, 0);
+            for (const SaSplit& sp : splits) is_split[sp.job] = 1;
+            for (int32_t j : todo)
+                if (!is_split[j]) queue.push_back(j);
+        }
+        const int nj = (int)queue.size();
         scr.ensure((size_t)std::max<int64_t>(scratch, 256));
         put(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob));
-        put(al->d_order.p, todo.data(), todo.size() * 4);
+        al->d_order.grow(queue.size());
+        put(al->d_order.p, queue.data(), queue.size() * 4);
         NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
         // per-slot scratch: word table, append_aligned stack, regions
         // SA_WAVES_PER_EU waves on each of the 4 SIMDs of the 256 CUs
@@ -1485,7 +2246,9 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         }
         A.defer = defer ? al->defer : 0;
         A.defer_rows = al->defer_rows;
-        if (defer) {
+        // deferred bad regions: of the long jobs (defer) and of every split job
+        const bool deferring = defer || !splits.empty();
+        if (deferring) {
             al->d_job_regions.grow((size_t)n_reg);
             al->d_job_nreg.grow(jobs.size());
             al->d_fin.grow(jobs.size());
@@ -1556,6 +2319,39 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.stage_bytes = o.aligner_type == 0 ? (int32_t)std::min<int64_t>(max_need, stage_cap & ~15ll) : 0;
         const size_t lds_bytes = (size_t)table_bytes + (size_t)A.stage_bytes;
         NPGX_REQUIRE(A.stage_bytes >= 0 && lds_bytes <= (size_t)LDS_PER_CU, NPGX_ERR_STATE, "LDS budget");
+        A.splits = nullptr;
+        A.segs = nullptr;
+        A.targets = nullptr;
+        A.seg_res = nullptr;
+        A.seg_wall = nullptr;
+        A.seg_done = nullptr;
+        A.seg_pool = nullptr;
+        if (!splits.empty()) {
+            al->d_splits.grow(splits.size());
+            al->d_segs.grow(segs.size());
+            al->d_ftasks.grow(ftasks.size());
+            al->d_targets.grow((size_t)n_tgt);
+            al->d_seg_res.grow(segs.size());
+            al->d_seg_wall.grow(2 * segs.size());
+            al->d_seg_done.grow(splits.size());
+            al->d_seg_pool.grow((size_t)seg_bytes);
+            put(al->d_splits.p, splits.data(), splits.size() * sizeof(SaSplit));
+            put(al->d_segs.p, segs.data(), segs.size() * sizeof(SaSeg));
+            put(al->d_ftasks.p, ftasks.data(), ftasks.size() * sizeof(int2));
+            NPGX_HIP(hipMemsetAsync(al->d_seg_done.p, 0, splits.size() * 4, st));
+            A.splits = al->d_splits.p;
+            A.segs = al->d_segs.p;
+            A.targets = al->d_targets.p;
+            A.seg_res = al->d_seg_res.p;
+            A.seg_wall = al->d_seg_wall.p;
+            A.seg_done = al->d_seg_done.p;
+            A.seg_pool = al->d_seg_pool.p;
+            size_t tf = al->timer.begin("align_split", st, 0.0, (int64_t)ftasks.size());
+            hipLaunchKernelGGL(k_split_find, dim3((unsigned)ftasks.size()), dim3(64), SPLIT_LDS, st, A,
+                               al->d_ftasks.p, (int)ftasks.size());
+            NPGX_HIP(hipGetLastError());
+            al->timer.end(tf, st);
+        }
         int64_t residues = 0;
         for (int32_t j : todo) residues += jsum[j];
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
@@ -1563,15 +2359,88 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
-        if (defer) {  // the deferred bad regions, then their jobs (both no-ops when nothing was deferred)
+        if (!splits.empty()) {  // the split jobs: chain, regions, deferred bad regions
+            ti = al->timer.begin("align_split_post", st, 0.0, (int64_t)splits.size());
+            hipLaunchKernelGGL(k_split_post, dim3((unsigned)splits.size()), dim3(POST_THREADS), POST_LDS, st, A,
+                               (int)POST_LDS);
+            NPGX_HIP(hipGetLastError());
+            al->timer.end(ti, st);
+        }
+        if (deferring) {  // the deferred bad regions, then their jobs (no-ops when nothing was deferred)
+            // jobs that may have deferred: the split ones and the long ones
+            int64_t n_fin = (int64_t)splits.size();
+            int64_t max_rc = 1;
+            {
+                std::vector<uint8_t> is_split(n_jobs, 0);
+                for (const SaSplit& sp : splits) is_split[sp.job] = 1;
+                for (int32_t j : todo) {
+                    const bool may = is_split[j] || (defer && jobs[j].cap >= al->defer && jobs[j].n >= al->defer_rows);
+                    if (!may) continue;
+                    n_fin += is_split[j] ? 0 : 1;
+                    max_rc = std::max<int64_t>(max_rc, jobs[j].reg_cap + 1);
+                }
+            }
+            const int lds_ints = (int)std::min<int64_t>(max_rc, 32768);
+            al->d_reg_dst.grow((size_t)n_reg + jobs.size());
             ti = al->timer.begin("align_sub", st, 0.0, 0);
             hipLaunchKernelGGL(k_align_sub, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
+            if (n_fin > 0) {
+                ti = al->timer.begin("align_fin_copy", st, 0.0, 0);
+                hipLaunchKernelGGL(k_fin_copy, dim3((unsigned)(n_fin * FIN_PARTS)), dim3(POST_THREADS),
+                                   (size_t)lds_ints * 4, st, A, lds_ints, al->d_reg_dst.p);
+                NPGX_HIP(hipGetLastError());
+                al->timer.end(ti, st);
+            }
             ti = al->timer.begin("align_finish", st, 0.0, 0);
             hipLaunchKernelGGL(k_align_finish, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
+        }
+        if (!splits.empty() && getenv("NPGX_SPLIT_DEBUG")) {  // diagnostic: sync states and segment results
+            std::vector<int32_t> tg((size_t)n_tgt);
+            std::vector<int4> sr(segs.size());
+            NPGX_HIP(hipMemcpyAsync(tg.data(), al->d_targets.p, tg.size() * 4, hipMemcpyDeviceToHost, st));
+            NPGX_HIP(hipMemcpyAsync(sr.data(), al->d_seg_res.p, sr.size() * 16, hipMemcpyDeviceToHost, st));
+            NPGX_HIP(hipStreamSynchronize(st));
+            for (const SaSplit& sp : splits) {
+                const int n = jobs[sp.job].n;
+                int valid = 0, ovf = 0, hits = 0;
+                for (int k = 1; k < sp.K; k++) valid += tg[sp.tgt + (int64_t)(k - 1) * n] >= 0;
+                std::string chain;
+                for (int k = 0; k < sp.K; k++) {
+                    const int4 r = sr[sp.seg0 + k];
+                    ovf += r.z;
+                    hits += r.x >= 0 && r.x < sp.K;
+                }
+                for (int k = 0, guard = 0; k < sp.K && k >= 0 && guard < 1000; guard++) {
+                    const int4 r = sr[sp.seg0 + k];
+                    chain += std::to_string(k) + "(" + std::to_string(r.y) + (r.z ? "!" : "") + ")>";
+                    if (r.x <= k) break;
+                    k = r.x;
+                }
+                fprintf(stderr, "split job %d n=%d K=%d maxlen=%d valid_states=%d hits=%d ovf=%d chain %s\n", sp.job,
+                        n, sp.K, jmax[sp.job], valid, hits, ovf, chain.c_str());
+            }
+            if (deferring) {  // sub-jobs: count and widths
+                unsigned long long al2[2];
+                NPGX_HIP(hipMemcpy(al2, al->d_alloc.p, 16, hipMemcpyDeviceToHost));
+                std::vector<SaSub> sb((size_t)al2[1]);
+                std::vector<int2> rs((size_t)al2[1]);
+                if (!sb.empty()) {
+                    NPGX_HIP(hipMemcpy(sb.data(), al->d_subs.p, sb.size() * sizeof(SaSub), hipMemcpyDeviceToHost));
+                    NPGX_HIP(hipMemcpy(rs.data(), al->d_sub_res.p, rs.size() * 8, hipMemcpyDeviceToHost));
+                }
+                std::vector<int> wd;
+                for (const int2& r : rs) wd.push_back(r.x);
+                std::sort(wd.begin(), wd.end());
+                long long tot = 0;
+                for (int x : wd) tot += x;
+                fprintf(stderr, "subs %zu total_cols %lld p50 %d p90 %d p99 %d max %d\n", wd.size(), tot,
+                        wd.empty() ? 0 : wd[wd.size() / 2], wd.empty() ? 0 : wd[wd.size() * 9 / 10],
+                        wd.empty() ? 0 : wd[wd.size() * 99 / 100], wd.empty() ? 0 : wd.back());
+            }
         }
         int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);
         NPGX_HIP(hipMemcpyAsync(pl, al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
@@ -1726,14 +2595,21 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         if (df && *df) a->defer = std::max(0, atoi(df));
         const char* dr = getenv("NPGX_ALIGN_DEFER_ROWS");
         if (dr && *dr) a->defer_rows = std::max(0, atoi(dr));
+        const char* sp = getenv("NPGX_ALIGN_SPLIT");
+        if (sp && *sp) a->split = std::max(0, atoi(sp));
         if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
             delete a;
             throw Error(NPGX_ERR_HIP, "stream creation failed");
         }
-        const void* kernels[3] = {(const void*)k_align_jobs, (const void*)k_align_sub, (const void*)k_align_finish};
+        // dynamic LDS of each kernel at most (k_split_post and k_fin_copy also
+        // have static LDS)
+        const std::pair<const void*, int> kernels[5] = {
+            {(const void*)k_align_jobs, (int)LDS_PER_CU}, {(const void*)k_align_sub, (int)LDS_PER_CU},
+            {(const void*)k_align_finish, (int)LDS_PER_CU}, {(const void*)k_split_post, (int)POST_LDS},
+            {(const void*)k_fin_copy, 32768 * 4}};
         bool lds_ok = true;
-        for (const void* k : kernels)
-            lds_ok = lds_ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_PER_CU) ==
+        for (const auto& k : kernels)
+            lds_ok = lds_ok && hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, k.second) ==
                                    hipSuccess;
         if (!lds_ok) {
             (void)hipStreamDestroy(a->stream);

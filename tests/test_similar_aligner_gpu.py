@@ -85,9 +85,14 @@ def _random_jobs(seed, count, nmax=20, lmax=300):
 def _check(jobs, kind="similar"):
     mode = "align_seqs" if kind == "similar" else "dummy"
     got = _aligner(kind).align(jobs)
-    for job, g in zip(jobs, got):
+    for j, (job, g) in enumerate(zip(jobs, got)):
         exp = orc.align(job, mode=mode)
-        assert g == exp, (job, g, exp)
+        if g != exp:
+            col = next((c for c in range(min(len(g[0]), len(exp[0]))) if any(x[c] != y[c] for x, y in zip(g, exp))),
+                       None) if g and exp else None
+            raise AssertionError("job %d (%d rows, lengths %s): %d columns vs %d expected, first difference at "
+                                 "column %s" % (j, len(job), [len(r) for r in job], len(g[0]) if g else 0,
+                                                len(exp[0]) if exp else 0, col))
 
 
 def test_kats_similar():
@@ -118,20 +123,28 @@ def test_random_families(seed):
 # the column and row counts from
 # which fix_bad_regions' re-alignments leave the job's workgroup and run as
 # sub-jobs of their own (0: never, 1: every alignment)
-@pytest.mark.parametrize("defer,rows", [("0", "0"), ("1", "0"), ("1000", "0"), ("1000", "4"), ("8000", "4")])
-def test_long_flanks(defer, rows, monkeypatch):
+# NPGX_ALIGN_SPLIT: long jobs are cut into segments of about this many
+# columns at sync states (0: never); small values put many sync states into
+# every job, including the high-divergence ones where the speculation misses
+@pytest.mark.parametrize("defer,rows,split", [("0", "0", "0"), ("1", "0", "0"), ("1000", "0", "0"),
+                                              ("1000", "4", "0"), ("8000", "4", "0"), ("8000", "4", "512"),
+                                              ("0", "0", "100"), ("1000", "4", "64")])
+def test_long_flanks(defer, rows, split, monkeypatch):
     monkeypatch.setenv("NPGX_ALIGN_DEFER", defer)
     monkeypatch.setenv("NPGX_ALIGN_DEFER_ROWS", rows)  # deferred only with at least this many rows
+    monkeypatch.setenv("NPGX_ALIGN_SPLIT", split)
     _check(_random_jobs(11, 40, nmax=17, lmax=1500))
 
 
-@pytest.mark.parametrize("defer,rows", [("0", "0"), ("1000", "0"), ("8000", "4")])
-def test_very_long_rows(defer, rows, monkeypatch):
+@pytest.mark.parametrize("defer,rows,split", [("0", "0", "0"), ("1000", "0", "0"), ("8000", "4", "0"),
+                                              ("8000", "4", "512"), ("1000", "0", "128")])
+def test_very_long_rows(defer, rows, split, monkeypatch):
     """Alignments of thousands of columns with hundreds of low-similarity
     regions (the LDS region reduction and its block minima) and some rows
     unrelated from part-way."""
     monkeypatch.setenv("NPGX_ALIGN_DEFER", defer)
     monkeypatch.setenv("NPGX_ALIGN_DEFER_ROWS", rows)
+    monkeypatch.setenv("NPGX_ALIGN_SPLIT", split)
     rng = np.random.default_rng(21)
     jobs = []
     for _ in range(12):
@@ -139,6 +152,26 @@ def test_very_long_rows(defer, rows, monkeypatch):
         L = int(rng.integers(4000, 12000))
         d = float(rng.choice([0.02, 0.05, 0.1]))
         jobs.append(_family(rng, n, L, d, tail_unrelated=float(rng.choice([0.0, 0.3]))))
+    _check(jobs)
+
+
+@pytest.mark.parametrize("split", ["64", "256"])
+def test_split_similar_families(split, monkeypatch):
+    """Long, highly similar families (the C2/C3 flank shape: the sync states
+    mostly hold) with short segments, and repeats inside the rows (a sync word
+    that is not unique in its window is skipped)."""
+    monkeypatch.setenv("NPGX_ALIGN_SPLIT", split)
+    rng = np.random.default_rng(31)
+    jobs = []
+    for _ in range(16):
+        n = int(rng.integers(2, 20))
+        L = int(rng.integers(2000, 9000))
+        jobs.append(_family(rng, n, L, float(rng.choice([0.005, 0.01, 0.02])), nrate=0.3))
+    unit = "".join("ATGC"[x] for x in rng.integers(0, 4, 150))
+    for _ in range(4):  # tandem repeats of a 150-mer between unique stretches
+        base = _family(rng, 1, 3000, 0.0)[0]
+        rows = _family(rng, int(rng.integers(3, 9)), 1, 0.0)
+        jobs.append([base[:1000] + unit * 8 + base[1000:] for _ in rows])
     _check(jobs)
 
 

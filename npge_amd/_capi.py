@@ -132,9 +132,14 @@ def device_count():
     return n.value
 
 
-def kernel_times(fn, handle, cap=64):
-    arr = (KernelTime * cap)()
+def kernel_times(fn, handle, cap=None):
+    """Every kernel-time record of the handle's last call (sized by a first
+    query unless `cap` is given)."""
     n = ctypes.c_int32(0)
+    if cap is None:
+        check(fn(handle, None, 0, ctypes.byref(n)))
+        cap = max(n.value, 1)
+    arr = (KernelTime * cap)()
     check(fn(handle, arr, cap, ctypes.byref(n)))
     return [dict(name=arr[i].name.decode(), ms=arr[i].ms, bytes=arr[i].bytes, units=arr[i].units)
             for i in range(min(n.value, cap))]

@@ -45,14 +45,19 @@ def anchor_loop_fast(eng, af=None):
     eng.set_blocks(sorted(eng.blocks(), key=block_order))
     cs = eng.conseq()
     css = _capi.SeqSet(cs, [""] * len(cs))  # ConSeq names = block names (empty here)
-    cons = BlockSetEngine(css)
+    # the pipe's ExtendLoopFast runs to convergence (set_max_iterations(-1),
+    # lua_lib.lua:697-699); DraftPangenome's cap of 10 does not apply here
+    cons = BlockSetEngine(css, max_iterations=-1)
     af.clear_used()
     anchors = anchor_blocks(af.find(css))
     cons.set_blocks(anchors)
-    cons.apply("DummyAligner").apply("FragmentsExtender").apply("Align").apply("ExtendLoopFast")
+    # ExtendAndAlign (lua_lib.lua:669-674), then ExtendLoopFast
+    cons.apply("DummyAligner").apply("FragmentsExtender --extend-length-portion:=0.5").apply("Align")
+    cons.apply("ExtendLoopFast")
+    loop_iterations = cons.stats()["iterations"]
     n_cons = len(cons.blocks())
     n_before = len(eng.blocks())
     eng.deconseq(cons)
     eng.apply("Align")
     return dict(consensus_sequences=len(cs), anchors=len(anchors), cons_blocks=n_cons,
-                mapped_blocks=len(eng.blocks()) - n_before)
+                mapped_blocks=len(eng.blocks()) - n_before, loop_iterations=loop_iterations)

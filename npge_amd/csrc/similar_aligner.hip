@@ -61,7 +61,13 @@ struct SaSplit {
     int64_t tgt;        // first int of its sync states (K - 1 states x n rows)
     int32_t seg0;       // its first segment task
     int32_t win;        // half-width of the sync word search window
+    int32_t sub;        // -1: the job's own rows; else the job's sub-job (a bad region) of this index
+    int32_t pad;
 };
+
+// split-state counters (device): the job splits are planned on the host, the
+// sub-job splits by k_plan_subs
+enum { SC_SPLITS, SC_SEGS, SC_TGT, SC_FIND, SC_QSEG, SC_QSUB, SC_POOL_LO, SC_POOL_HI, SC_N };
 
 struct SaSeg {
     int32_t split;      // index into splits
@@ -123,8 +129,16 @@ struct SaArgs {
     int32_t* targets;          // sync states (k_split_find)
     int4* seg_res;             // per segment: next segment (K: ran to the end, -1: idle), columns, overflow
     int64_t* seg_wall;         // per segment: wall clock at start and end (job statistics)
-    unsigned int* seg_done;    // per split job: segments finished
     unsigned char* seg_pool;
+    // sub-job splits (k_plan_subs): capacities of the arrays above and the
+    // sub-job queue (segment tasks first, then whole sub-jobs)
+    unsigned int* sctr;
+    int32_t* qseg;
+    int32_t* qsub;
+    int2* ftasks;
+    int32_t split_len;         // segment length for a job of 16 rows (0: no splitting)
+    int32_t cap_splits, cap_segs;
+    int64_t cap_tgt, cap_find, cap_pool;
 };
 
 // number of columns c in [c0, c1) identical over all rows (score_of :416-426)
@@ -857,18 +871,35 @@ __device__ __forceinline__ int fin_width(const SaArgs& a, int4 rg) {
     return res.y > rg.w ? res.x : len;  // more identical columns: the re-alignment (score_of :445-455)
 }
 
-// k_align_sub: every bad region of every deferred job, one wave each
+// k_align_sub: every bad region of every deferred job, one wave each; with a
+// plan (k_plan_subs) the segments of the split sub-jobs first, then the other
+// sub-jobs
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_sub(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
     SlotEnv e = slot_env(a, lds_u64);
     uint32_t epoch = next_epoch(a), lepoch = 0;
     const unsigned int n_sub = (unsigned int)a.alloc[1];
+    const bool planned = a.sctr != nullptr;
+    const unsigned int nseg = planned ? a.sctr[SC_QSEG] : 0u;
+    const unsigned int nq = planned ? nseg + a.sctr[SC_QSUB] : n_sub;
     while (true) {
-        unsigned int sn = 0;
-        if (lane == 0) sn = atomicAdd(&a.counters[0], 1u);
-        sn = bcast(sn, 0);
-        if (sn >= n_sub) break;
+        unsigned int qn = 0;
+        if (lane == 0) qn = atomicAdd(&a.counters[0], 1u);
+        qn = bcast(qn, 0);
+        if (qn >= nq) break;
+        const bool seg = qn < nseg;
+        const int seg_t = seg ? a.qseg[qn] : -1;
+        SaSeg sg{};
+        SaSplit sp{};
+        int sn;
+        if (seg) {
+            sg = a.segs[seg_t];
+            sp = a.splits[sg.split];
+            sn = sp.sub;
+        } else {
+            sn = planned ? a.qsub[qn - nseg] : (int)qn;
+        }
         const SaSub d = a.subs[sn];
         const SaJob job = a.jobs[d.job];
         const int n = job.n, cap = job.cap;
@@ -878,19 +909,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
         w.act = lane < n;
         char* C = (char*)(a.scratch + job.scratch) + 2ll * n * cap;
+        const int* T = seg ? a.targets + sp.tgt : nullptr;  // sync state k >= 1 at T[(k-1)*n + row]
+        const int start = (seg && sg.k > 0 && w.act) ? T[(sg.k - 1) * n + lane] : 0;
+        const bool idle = seg && any_lane(w, start < 0);
         View v{nullptr, 0, 1};
-        if (w.act) {
-            v.p = C + (size_t)lane * cap + d.x;
-            v.len = ((const int*)(a.pool + d.out_off))[lane];
+        if (w.act && !idle) {
+            v.p = C + (size_t)lane * cap + d.x + start;
+            v.len = ((const int*)(a.pool + d.out_off))[lane] - start;
         }
-        stage_rows(v, n, e.stage, a.stage_bytes);
-        char* out = (char*)(a.pool + d.out_off + 256);
-        Proc pr(w, a.P, e.S, out, d.out_cap, epoch, lepoch);
-        const int Lc = pr.run(v, 0);
-        const bool ovf = any_lane(w, pr.ovf);
+        char* out = seg ? (char*)(a.seg_pool + sg.out) : (char*)(a.pool + d.out_off + 256);
+        Proc pr(w, a.P, e.S, out, seg ? sg.cap : d.out_cap, epoch, lepoch);
+        int Lc = 0;
+        bool ovf = false;
+        if (!idle) {
+            stage_rows(v, n, e.stage, a.stage_bytes);
+            if (seg) pr.set_targets(T, sg.k, sp.K - 1, start);
+            Lc = pr.run(v, 0);
+            ovf = any_lane(w, pr.ovf);
+        }
         __syncthreads();
-        const int after = ovf ? 0 : count_equal_cols(w, out, d.out_cap, 0, Lc, nullptr);
-        if (lane == 0) a.sub_res[sn] = make_int2(ovf ? -1 : Lc, after);
+        if (seg) {
+            if (lane == 0)
+                a.seg_res[seg_t] = idle ? make_int4(-1, 0, 0, 0)
+                                        : make_int4(pr.stop ? pr.tm + 1 : sp.K, Lc, ovf ? 1 : 0, 0);
+        } else {
+            const int after = ovf ? 0 : count_equal_cols(w, out, d.out_cap, 0, Lc, nullptr);
+            if (lane == 0) a.sub_res[sn] = make_int2(ovf ? -1 : Lc, after);
+        }
         epoch = pr.epoch;
         lepoch = pr.lepoch;
         __syncthreads();
@@ -975,6 +1020,27 @@ static constexpr int SPLIT_HT = 2048;    // LDS hash table entries (> 1.75 x SPL
 static constexpr int SPLIT_KMAX = 128;   // segments per job at most
 static constexpr size_t SPLIT_LDS = (size_t)SPLIT_HT * 12 + (size_t)64 * SPLIT_C * 2 + SPLIT_SPAN + SPLIT_W + 80;
 
+// segment length of a job of n rows: per-column cost grows with the rows, so
+// few-row jobs take longer segments (the sync state search costs the same)
+__host__ __device__ __forceinline__ int split_len_for(int split, int n) {
+    const int f = n >= 16 ? 1 : 16 / (n > 0 ? n : 1);
+    return split * (f > 8 ? 8 : f);
+}
+
+// row `lane` of a split problem: the job's input row, or the gap-filtered
+// reversed bad-region row of one of its sub-jobs (in the job's C)
+__device__ __forceinline__ void split_row(const SaArgs& a, const SaSplit& sp, const SaJob& job, int lane,
+                                          const char*& p, int& len) {
+    if (sp.sub < 0) {
+        p = a.rows + a.row_off[job.row0 + lane];
+        len = a.row_len[job.row0 + lane];
+    } else {
+        const SaSub d = a.subs[sp.sub];
+        p = (const char*)(a.scratch + job.scratch) + (2 * (size_t)job.n + lane) * job.cap + d.x;
+        len = ((const int*)(a.pool + d.out_off))[lane];
+    }
+}
+
 __device__ __forceinline__ uint32_t base2(uint32_t c) {  // A C G T -> 0..3, anything else 4
     return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
 }
@@ -989,21 +1055,23 @@ __device__ __forceinline__ uint32_t base2(uint32_t c) {  // A C G T -> 0..3, any
 // its word -- inside an identical stretch of at least 12 columns, which the
 // walk crosses column by column when it is in step there.  None survives: -1
 // in every row (segment t+1 idles).
-__global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, int n_tasks) {
+__global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, int n_tasks, int task0) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
     uint32_t* hkey = lds_w;                        // tag << 24 | word
     uint32_t* hlo = hkey + SPLIT_HT;               // max of tag << 16 | (0xFFFF - first position)
     uint32_t* hhi = hlo + SPLIT_HT;                // max of tag << 16 | last position
     uint16_t* P = (uint16_t*)(hhi + SPLIT_HT);     // [row][candidate] window offset of its occurrence
     unsigned char* ch = (unsigned char*)(P + 64 * SPLIT_C);
-    const int b = blockIdx.x;
-    if (b >= n_tasks) return;
+    if (n_tasks < 0) n_tasks = (int)min(a.sctr[SC_FIND], (unsigned int)a.cap_find);  // the sub-job pass
+    for (int b = task0 + blockIdx.x; b < n_tasks; b += gridDim.x) {
     const int lane = threadIdx.x;
     const int2 tk = tasks[b];
+    if (tk.x < 0) continue;  // (a sub-job k_plan_subs could not split)
     const SaSplit sp = a.splits[tk.x];
     const SaJob job = a.jobs[sp.job];
     const int n = job.n, t = tk.y, R = min(sp.win, SPLIT_RMAX);
     const int span = 2 * R + SPLIT_C + 1;
+    __syncthreads();
     for (int e = lane; e < SPLIT_HT; e += 64) {
         hkey[e] = 0u;
         hlo[e] = 0u;
@@ -1017,8 +1085,9 @@ __global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, 
     unsigned char nx[PER];
     int lo_next = 0;
     {
-        const int li = a.row_len[job.row0];
-        const char* ri = a.rows + a.row_off[job.row0];
+        const char* ri;
+        int li;
+        split_row(a, sp, job, 0, ri, li);
         lo_next = (int)((int64_t)li * (t + 1) / sp.K) - R;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
@@ -1033,8 +1102,9 @@ __global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, 
         for (int u = 0; u < PER; u++) ch[u * 64 + lane] = nx[u];
         __syncthreads();
         if (i + 1 < n) {
-            const int li = a.row_len[job.row0 + i + 1];
-            const char* ri = a.rows + a.row_off[job.row0 + i + 1];
+            const char* ri;
+            int li;
+            split_row(a, sp, job, i + 1, ri, li);
             lo_next = (int)((int64_t)li * (t + 1) / sp.K) - R;
 #pragma unroll
             for (int u = 0; u < PER; u++) {
@@ -1120,12 +1190,15 @@ __global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, 
     if (lane < n) {
         int v = -1;
         if (best >= 0) {
-            const int li = a.row_len[job.row0 + lane];
+            const char* ri;
+            int li;
+            split_row(a, sp, job, lane, ri, li);
             const int lo = (int)((int64_t)li * (t + 1) / sp.K) - R;
             v = lo + (int)P[lane * SPLIT_C + best] + SPLIT_W / 2;
         }
         out[lane] = v;
     }
+    }  // tasks
 }
 
 // ---------------------------------------------------- split jobs after their segments
@@ -1488,6 +1561,137 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_b
         a.fin[atomicAdd(&a.counters[1], 1u)] = j;
         a.job_len[j] = L0;
         a.job_status[j] = 3;
+    }
+}
+
+// One thread per sub-job (after k_align_jobs and k_split_post created them):
+// a sub-job whose longest row spans at least two segments is split like the
+// long jobs -- its sync states by k_split_find, its segments ahead of the
+// whole sub-jobs in k_align_sub's queue, its chain by k_sub_post.  The split
+// arrays are bounded; a sub-job that does not fit them runs whole.
+__global__ __launch_bounds__(256) void k_plan_subs(SaArgs a) {
+    const unsigned int n_sub = (unsigned int)a.alloc[1];
+    unsigned long long* pool_ctr = (unsigned long long*)(a.sctr + SC_POOL_LO);
+    for (unsigned int sn = blockIdx.x * blockDim.x + threadIdx.x; sn < n_sub; sn += gridDim.x * blockDim.x) {
+        const SaSub d = a.subs[sn];
+        const SaJob job = a.jobs[d.job];
+        const int n = job.n;
+        const int* lens = (const int*)(a.pool + d.out_off);
+        int mx = 0;
+        for (int i = 0; i < n; i++) mx = max(mx, lens[i]);
+        const int K = (a.split_len > 0 && n >= 2) ? min(SPLIT_KMAX, mx / split_len_for(a.split_len, n)) : 1;
+        bool ok = K >= 2 && mx >= 4 * SPLIT_W;
+        if (ok) {
+            const int win = min(SPLIT_RMAX, 64 + mx / 128);
+            auto seg_cap = [&](int k) {  // the suffix bound, at most the sub-job's own output
+                const int64_t rest = mx - (int64_t)mx * k / K + win;
+                return (int)min((int64_t)d.out_cap, (2 * rest + 64 + 15) & ~15ll);
+            };
+            int64_t bytes = 0;
+            for (int k = 0; k < K; k++) bytes += ((int64_t)n * seg_cap(k) + 255) & ~255ll;
+            const unsigned long long p0 = atomicAdd(pool_ctr, (unsigned long long)bytes);
+            const unsigned int s0 = atomicAdd(&a.sctr[SC_SEGS], (unsigned int)K);
+            const unsigned int t0 = atomicAdd(&a.sctr[SC_TGT], (unsigned int)((K - 1) * n));
+            const unsigned int f0 = atomicAdd(&a.sctr[SC_FIND], (unsigned int)(K - 1));
+            const unsigned int si = atomicAdd(&a.sctr[SC_SPLITS], 1u);
+            ok = p0 + bytes <= (unsigned long long)a.cap_pool && s0 + K <= (unsigned int)a.cap_segs &&
+                 (int64_t)t0 + (int64_t)(K - 1) * n <= a.cap_tgt && (int64_t)f0 + K - 1 <= a.cap_find &&
+                 si < (unsigned int)a.cap_splits;
+            for (int t = 0; t + 1 < K; t++)  // (allocated find tasks are written either way)
+                if ((int64_t)f0 + t < a.cap_find) a.ftasks[f0 + t] = ok ? make_int2((int)si, t) : make_int2(-1, -1);
+            if (si < (unsigned int)a.cap_splits) {
+                SaSplit sp;
+                sp.job = d.job;
+                sp.K = ok ? K : 0;
+                sp.tgt = t0;
+                sp.seg0 = (int32_t)s0;
+                sp.win = win;
+                sp.sub = (int32_t)sn;
+                sp.pad = 0;
+                ((SaSplit*)a.splits)[si] = sp;
+            }
+            if (ok) {
+                int64_t off = (int64_t)p0;
+                const unsigned int q0 = atomicAdd(&a.sctr[SC_QSEG], (unsigned int)K);
+                for (int k = 0; k < K; k++) {
+                    SaSeg g;
+                    g.split = (int32_t)si;
+                    g.k = k;
+                    g.cap = seg_cap(k);
+                    g.pad = 0;
+                    g.out = off;
+                    off += ((int64_t)n * g.cap + 255) & ~255ll;
+                    ((SaSeg*)a.segs)[s0 + k] = g;
+                    a.qseg[q0 + k] = (int32_t)(s0 + k);
+                }
+            }
+        }
+        if (!ok) a.qsub[atomicAdd(&a.sctr[SC_QSUB], 1u)] = (int32_t)sn;
+    }
+}
+
+// One workgroup per split sub-job (split index from `first`): the chain of its
+// segments into the sub-job's output (rows of out_cap) and its identical
+// columns (score_of after the re-alignment) -- what k_align_sub writes for a
+// whole sub-job; a chain that overflowed or does not fit: (-1, 0).
+__global__ __launch_bounds__(POST_THREADS) void k_sub_post(SaArgs a, int first) {
+    __shared__ int pk[SPLIT_KMAX], pcols[SPLIT_KMAX], pdst[SPLIT_KMAX];
+    __shared__ int s_np, s_L, s_fail, s_scan[POST_THREADS / 64];
+    const int tid = threadIdx.x;
+    const int last = (int)min(a.sctr[SC_SPLITS], (unsigned int)a.cap_splits);
+    for (int si = first + blockIdx.x; si < last; si += gridDim.x) {
+        const SaSplit sp = a.splits[si];
+        if (sp.K < 2) continue;
+        const SaSub d = a.subs[sp.sub];
+        const int n = a.jobs[d.job].n;
+        __syncthreads();
+        if (tid == 0) {
+            int k = 0, col = 0, np = 0, fail = 0;
+            while (k < sp.K) {
+                const int4 r = a.seg_res[sp.seg0 + k];
+                if (r.x <= k || r.z || col + r.y > d.out_cap) {
+                    fail = 1;
+                    break;
+                }
+                pk[np] = sp.seg0 + k;
+                pcols[np] = r.y;
+                pdst[np] = col;
+                np++;
+                col += r.y;
+                k = r.x;
+            }
+            s_np = np;
+            s_L = col;
+            s_fail = fail;
+        }
+        __syncthreads();
+        if (s_fail) {
+            if (tid == 0) a.sub_res[sp.sub] = make_int2(-1, 0);
+            continue;
+        }
+        char* out = (char*)(a.pool + d.out_off + 256);
+        int same = 0;
+        for (int p = 0; p < s_np; p++) {
+            const SaSeg g = a.segs[pk[p]];
+            const char* src = (const char*)(a.seg_pool + g.out);
+            const int cols = pcols[p], d0 = pdst[p];
+            for (int c = 4 * tid; c < cols; c += 4 * POST_THREADS) {
+                const int nb = min(4, cols - c);
+                const uint32_t x0 = *(const uint32_t*)(src + c);
+                uint32_t diff = 0;
+                for (int b = 0; b < nb; b++) out[d0 + c + b] = (char)(x0 >> (8 * b));
+                for (int r = 1; r < n; r++) {
+                    const uint32_t x = *(const uint32_t*)(src + (size_t)r * g.cap + c);
+                    diff |= x ^ x0;
+                    char* dr = out + (size_t)r * d.out_cap + d0 + c;
+                    for (int b = 0; b < nb; b++) dr[b] = (char)(x >> (8 * b));
+                }
+                for (int b = 0; b < nb; b++) same += !((diff >> (8 * b)) & 0xFFu);
+            }
+        }
+        int tot = 0;
+        block_scan_excl(same, &tot, s_scan);
+        if (tid == 0) a.sub_res[sp.sub] = make_int2(s_L, tot);
     }
 }
 
@@ -1970,7 +2174,8 @@ struct npgx_aligner {
     DevBuf<int32_t> d_targets;
     DevBuf<int4> d_seg_res;
     DevBuf<int64_t> d_seg_wall;
-    DevBuf<unsigned int> d_seg_done;
+    DevBuf<int32_t> d_qseg, d_qsub;
+    DevBuf<unsigned int> d_sctr;
     DevBuf<unsigned char> d_seg_pool;
     DevBuf<int> d_reg_dst;  // k_fin_copy's region offsets when they do not fit its LDS
     // last result
@@ -2140,14 +2345,16 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             for (int32_t j : todo) {
                 const SaJob& J = jobs[j];
                 const int mx = jmax[j];
-                const int K = std::min(SPLIT_KMAX, mx / al->split);
+                const int K = std::min(SPLIT_KMAX, mx / split_len_for(al->split, J.n));
                 if (J.n < 2 || K < 2 || mx < 4 * SPLIT_W) continue;
                 SaSplit sp;
                 sp.job = j;
                 sp.K = K;
                 sp.tgt = n_tgt;
                 sp.seg0 = (int32_t)segs.size();
-                sp.win = std::min(SPLIT_RMAX, 64 + mx / 64);
+                sp.win = std::min(SPLIT_RMAX, 64 + mx / 128);
+                sp.sub = -1;
+                sp.pad = 0;
                 n_tgt += (int64_t)(K - 1) * J.n;
                 for (int k = 0; k < K; k++) {
                     SaSeg g;
@@ -2324,33 +2531,59 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.targets = nullptr;
         A.seg_res = nullptr;
         A.seg_wall = nullptr;
-        A.seg_done = nullptr;
         A.seg_pool = nullptr;
-        if (!splits.empty()) {
-            al->d_splits.grow(splits.size());
-            al->d_segs.grow(segs.size());
-            al->d_ftasks.grow(ftasks.size());
-            al->d_targets.grow((size_t)n_tgt);
-            al->d_seg_res.grow(segs.size());
-            al->d_seg_wall.grow(2 * segs.size());
-            al->d_seg_done.grow(splits.size());
-            al->d_seg_pool.grow((size_t)seg_bytes);
-            put(al->d_splits.p, splits.data(), splits.size() * sizeof(SaSplit));
-            put(al->d_segs.p, segs.data(), segs.size() * sizeof(SaSeg));
-            put(al->d_ftasks.p, ftasks.data(), ftasks.size() * sizeof(int2));
-            NPGX_HIP(hipMemsetAsync(al->d_seg_done.p, 0, splits.size() * 4, st));
+        A.sctr = nullptr;
+        A.qseg = nullptr;
+        A.qsub = nullptr;
+        A.ftasks = nullptr;
+        A.split_len = o.aligner_type == 0 ? al->split : 0;
+        A.cap_splits = A.cap_segs = 0;
+        A.cap_tgt = A.cap_find = A.cap_pool = 0;
+        const int n_job_splits = (int)splits.size(), n_job_find = (int)ftasks.size();
+        const bool split_subs = deferring && A.split_len > 0;
+        if (!splits.empty() || split_subs) {
+            // the job splits (host plan) and room for the sub-job splits (k_plan_subs)
+            A.cap_splits = n_job_splits + (split_subs ? (int32_t)std::min<int64_t>(n_sub_max, 1 << 20) : 0);
+            A.cap_segs = (int32_t)segs.size() + (split_subs ? (1 << 17) : 0);
+            A.cap_tgt = n_tgt + (split_subs ? (1ll << 22) : 0);
+            A.cap_find = n_job_find + (split_subs ? (1ll << 17) : 0);
+            A.cap_pool = seg_bytes + (split_subs ? std::max<int64_t>(256ll << 20, 4 * (int64_t)(scratch + (16 << 20))) : 0);
+            al->d_splits.grow((size_t)std::max(1, A.cap_splits));
+            al->d_segs.grow((size_t)std::max(1, A.cap_segs));
+            al->d_ftasks.grow((size_t)std::max<int64_t>(1, A.cap_find));
+            al->d_targets.grow((size_t)std::max<int64_t>(1, A.cap_tgt));
+            al->d_seg_res.grow((size_t)std::max(1, A.cap_segs));
+            al->d_seg_wall.grow(2 * (size_t)std::max(1, A.cap_segs));
+            al->d_seg_pool.grow((size_t)std::max<int64_t>(256, A.cap_pool));
+            al->d_qseg.grow((size_t)std::max(1, A.cap_segs));
+            al->d_qsub.grow((size_t)std::max<int64_t>(1, n_sub_max));
+            al->d_sctr.ensure(SC_N);
+            if (!splits.empty()) {
+                put(al->d_splits.p, splits.data(), splits.size() * sizeof(SaSplit));
+                put(al->d_segs.p, segs.data(), segs.size() * sizeof(SaSeg));
+                put(al->d_ftasks.p, ftasks.data(), ftasks.size() * sizeof(int2));
+            }
+            const uint32_t sc[SC_N] = {(uint32_t)n_job_splits, (uint32_t)segs.size(), (uint32_t)n_tgt,
+                                       (uint32_t)n_job_find, 0u, 0u, (uint32_t)seg_bytes,
+                                       (uint32_t)((uint64_t)seg_bytes >> 32)};
+            put(al->d_sctr.p, sc, sizeof(sc));
             A.splits = al->d_splits.p;
             A.segs = al->d_segs.p;
             A.targets = al->d_targets.p;
             A.seg_res = al->d_seg_res.p;
             A.seg_wall = al->d_seg_wall.p;
-            A.seg_done = al->d_seg_done.p;
             A.seg_pool = al->d_seg_pool.p;
-            size_t tf = al->timer.begin("align_split", st, 0.0, (int64_t)ftasks.size());
-            hipLaunchKernelGGL(k_split_find, dim3((unsigned)ftasks.size()), dim3(64), SPLIT_LDS, st, A,
-                               al->d_ftasks.p, (int)ftasks.size());
-            NPGX_HIP(hipGetLastError());
-            al->timer.end(tf, st);
+            A.sctr = al->d_sctr.p;
+            A.qseg = al->d_qseg.p;
+            A.qsub = al->d_qsub.p;
+            A.ftasks = al->d_ftasks.p;
+            if (n_job_find > 0) {
+                size_t tf = al->timer.begin("align_split", st, 0.0, (int64_t)n_job_find);
+                hipLaunchKernelGGL(k_split_find, dim3((unsigned)n_job_find), dim3(64), SPLIT_LDS, st, A,
+                                   al->d_ftasks.p, n_job_find, 0);
+                NPGX_HIP(hipGetLastError());
+                al->timer.end(tf, st);
+            }
         }
         int64_t residues = 0;
         for (int32_t j : todo) residues += jsum[j];
@@ -2382,10 +2615,25 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             }
             const int lds_ints = (int)std::min<int64_t>(max_rc, 32768);
             al->d_reg_dst.grow((size_t)n_reg + jobs.size());
+            if (split_subs) {  // the long sub-jobs: plan, sync states
+                ti = al->timer.begin("align_sub_split", st, 0.0, 0);
+                hipLaunchKernelGGL(k_plan_subs, dim3(256), dim3(256), 0, st, A);
+                NPGX_HIP(hipGetLastError());
+                hipLaunchKernelGGL(k_split_find, dim3(2048), dim3(64), SPLIT_LDS, st, A, al->d_ftasks.p, -1,
+                                   n_job_find);
+                NPGX_HIP(hipGetLastError());
+                al->timer.end(ti, st);
+            }
             ti = al->timer.begin("align_sub", st, 0.0, 0);
             hipLaunchKernelGGL(k_align_sub, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
+            if (split_subs) {  // the split sub-jobs' chains
+                ti = al->timer.begin("align_sub_post", st, 0.0, 0);
+                hipLaunchKernelGGL(k_sub_post, dim3(512), dim3(POST_THREADS), 0, st, A, n_job_splits);
+                NPGX_HIP(hipGetLastError());
+                al->timer.end(ti, st);
+            }
             if (n_fin > 0) {
                 ti = al->timer.begin("align_fin_copy", st, 0.0, 0);
                 hipLaunchKernelGGL(k_fin_copy, dim3((unsigned)(n_fin * FIN_PARTS)), dim3(POST_THREADS),

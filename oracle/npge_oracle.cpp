@@ -1760,7 +1760,7 @@ static int filter_block(const std::vector<BSeq>& seqs, BBlock& b, const FilterOp
 struct PipelineOpts {
     SimilarAlignerImpl im;
     int extend_length = 100;            // MIN_LENGTH
-    int64_t portion_x1e4 = 5000;        // --extend-length-portion:=0.5
+    int64_t portion_x1e4 = 0;           // FragmentsExtender --extend-length-portion (FragmentsExtender.cpp:28-30: 0.0)
     int fix_min_fragment = 100;
     int64_t fix_min_identity_x1e4 = 9000;
     int max_iterations = 10;
@@ -1882,12 +1882,14 @@ static void extend_loop_fast(BlockSetO& bs, const PipelineOpts& o, PipelineStats
         std::sort(mu_hashes.begin(), mu_hashes.end());
         mu_hashes.erase(std::unique(mu_hashes.begin(), mu_hashes.end()), mu_hashes.end());
         // ExtendAndFix: FragmentsExtender --extend-length-portion:=0.5, FixEnds
+        // (lua_lib.lua:690-695; ":=" fixes the value whatever the options)
+        const int64_t extend_and_fix_portion = 5000;
         std::vector<int64_t> aligned((size_t)std::max(o.workers, 1), 0);
         std::vector<BBlock> outs(work.size());
         std::vector<int> res(work.size(), 0);
         for_blocks(work.size(), o.workers, [&](size_t i, int t) {
             BBlock& b = work[i];
-            fragments_extender(seqs, b, o.extend_length, o.portion_x1e4, o.im, &aligned[(size_t)t]);
+            fragments_extender(seqs, b, o.extend_length, extend_and_fix_portion, o.im, &aligned[(size_t)t]);
             if (b.f.empty() || !b.f[0].has_row) return;  // FixEnds asserts alignment; anchors have rows
             res[i] = fix_ends(seqs, b, o.fix_min_fragment, o.fix_min_identity_x1e4, outs[i]);
         });

@@ -276,7 +276,7 @@ def align(rows, mode="similar", params=DEFAULT_SA, return_past_end=False):
 
 # ---------------------------------------------------------------- block sets
 PIPELINE_DEFAULTS = dict(
-    extend_length=100, portion_x1e4=5000, fix_min_fragment=100, fix_min_identity_x1e4=9000,
+    extend_length=100, portion_x1e4=0, fix_min_fragment=100, fix_min_identity_x1e4=9000,
     max_iterations=10, filter_min_fragment=100, filter_min_block=2, filter_frame_length=100,
     filter_min_end=10, filter_min_identity_x1e4=9000, filter_find_subblocks=1, do_filter=1,
     mismatch_check=1, gap_check=2, aligned_check=10, min_length=100, min_identity_x1e4=9000,

@@ -44,12 +44,15 @@ def _oracle_loop(o):
     o.apply("Rest")
     o.set_blocks(sorted(o.blocks(), key=block_order))
     cs = o.conseq()
-    oc = orc.BlockSetOracle(cs, [""] * len(cs))
+    # ExtendAndAlign's FragmentsExtender --extend-length-portion:=0.5, and the
+    # pipe's ExtendLoopFast to convergence (max_iterations -1)
+    oc = orc.BlockSetOracle(cs, [""] * len(cs), portion_x1e4=5000, max_iterations=-1)
     oc.set_blocks(anchor_blocks(orc.AnchorFinder().run(cs, [""] * len(cs))))
     for op in ("DummyAligner", "FragmentsExtender", "MetaAligner", "ExtendLoopFast"):
         oc.apply(op)
     o.deconseq(oc)
     o.apply("MetaAligner")
+    return oc.stats()
 
 
 @pytest.mark.parametrize("cfg", ["tiny", "small"])
@@ -63,7 +66,44 @@ def test_anchor_loop_fast(cfg):
     eng = _engine(seqs, names, start)
     st = anchor_loop_fast(eng, AnchorFinder())
     o.set_blocks(start)
-    _oracle_loop(o)
+    ost = _oracle_loop(o)
     assert st["consensus_sequences"] > len(start)
     assert st["anchors"] > 0 and st["mapped_blocks"] > 0
+    assert st["loop_iterations"] == ost["iterations"]
     assert canon(eng.blocks()) == canon(o.blocks())
+
+
+def test_extend_loop_to_convergence():
+    """ExtendLoopFast with max_iterations -1 (the AnchorLoopFast pipe's
+    set_max_iterations(-1)) runs past DraftPangenome's cap of 10 until the
+    block set repeats; engine and oracle agree on blocks and iterations."""
+    from npge_amd import _capi
+    from npge_amd.blockset import BlockSetEngine
+    from npge_amd.anchor_loop import anchor_blocks
+    names, seqs = synth.genome_set("small")  # converges after 14 iterations
+    anchors = anchor_blocks(orc.AnchorFinder().run(seqs, names))
+    eng = BlockSetEngine(_capi.SeqSet(seqs, names), max_iterations=-1).set_blocks(anchors)
+    o = orc.BlockSetOracle(seqs, names, max_iterations=-1)
+    o.set_blocks(anchors)
+    for se, so in (("RemoveNonStem --exact", "RemoveNonStem"), ("DummyAligner", "DummyAligner"),
+                   ("ExtendLoopFast", "ExtendLoopFast")):
+        eng.apply(se)
+        o.apply(so)
+    assert eng.stats()["iterations"] == o.stats()["iterations"] > 10
+    assert canon(eng.blocks()) == canon(o.blocks())
+
+
+def test_fragments_extender_portion_option():
+    """The standalone FragmentsExtender defaults to extend-length-portion 0
+    (FragmentsExtender.cpp:28-30); "--extend-length-portion:=0.5" is the
+    ExtendAndAlign / ExtendAndFix setting."""
+    names, seqs = synth.genome_set("tiny")
+    o = orc.BlockSetOracle(seqs, names)
+    o.apply("DraftPangenome")
+    start = o.blocks()
+    for opt, portion in (("", 0), (" --extend-length-portion:=0.5", 5000), (" --extend-length-portion=0.25", 2500)):
+        eng = _engine(seqs, names, start).apply("FragmentsExtender" + opt)
+        ref = orc.BlockSetOracle(seqs, names, portion_x1e4=portion)
+        ref.set_blocks(start)
+        ref.apply("FragmentsExtender")
+        assert canon(eng.blocks()) == canon(ref.blocks())

@@ -35,6 +35,8 @@ def parse():
     ap.add_argument("--config", default="C3",
                     help="synthetic genome set (npge_amd/synth.py); C3 = the 17-genome ≥50x target config")
     ap.add_argument("--mode", choices=("replicas", "sharded"), default="replicas")
+    ap.add_argument("--anchor-loop", action="store_true",
+                    help="each step also runs one AnchorLoopFast after DraftPangenome (lua_lib.lua:741-758)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -73,7 +75,7 @@ def main():
     if sharded:
         from npge_amd.comm import TorchComm
         comm = TorchComm(dist, staging="cuda")
-    job = pipeline.BlockBuild(ss, names, seqs, comm=comm)
+    job = pipeline.BlockBuild(ss, names, seqs, comm=comm, anchor_loop=args.anchor_loop)
 
     def step():
         return job.run()

@@ -267,6 +267,11 @@ typedef struct {
      * sent to goodSlices, 3 blocks after Filter, 4 blocks into OverlaplessUnion
      * (all iterations), 5 of them rejected, 6 block hashes computed */
     int64_t counters[8];
+    /* AnchorLoopFast: 0 consensus sequences, 1 anchor blocks on them, 2
+     * consensus blocks after the pipe's ExtendLoopFast, 3 blocks DeConSeq
+     * added, 4 the consensus ExtendLoopFast's iterations, 5 consensus blocks
+     * MoveUnchanged dropped */
+    int64_t loop[8];
 } npgx_bb_stats;
 
 void npgx_bb_default_options(npgx_bb_options* o);

@@ -1,24 +1,23 @@
-"""AnchorLoopFast (src/algo/lua_lib.lua:741-756) on the HIP engine:
+"""AnchorLoopFast (src/algo/lua_lib.lua:741-758) on the HIP engine:
 
     Filter; Rest target=target other=target; ConSeq target=cons other=target;
-    AnchorFinder target=cons; DummyAligner target=cons;
-    ExtendAndAlign target=cons (FragmentsExtender --extend-length-portion:=0.5,
-    Align); ExtendLoopFast target=cons; DeConSeq target=target other=cons;
-    Align; Clear target=cons
+    AnchorFinder target=cons; MoveUnchanged target=null other=cons;
+    DummyAligner target=cons; ExtendAndAlign target=cons (FragmentsExtender
+    --extend-length-portion:=0.5, Align); ExtendLoopFast target=cons (to
+    convergence); DeConSeq target=target other=cons; Align; Clear target=cons
 
 AnchorFinder runs on the consensus sequences of the current blocks (and the
 uncovered stretches Rest adds), the anchors are grown into aligned blocks on
 those consensuses and DeConSeq maps them back onto the genomes, where they are
-appended to the blocks.  The pipe's `MoveUnchanged target=null other=cons`
-step drops cons blocks whose hash an earlier run of the same pipe saw; one run
-(this function) has no earlier run, so it is a no-op here.  Every step is the
-engine's (GPU kernels + native host code); nothing falls back to the CPU.
+appended to the blocks.  The whole pipe is one engine call
+(``npgx_blockset_apply(b, "AnchorLoopFast", af)``): the consensus sequences
+get a device sequence set and an engine of their own inside the library, and
+no block list crosses into Python.  Like the reference's pipe object, the
+AnchorFinder handle (its used-hash set) and the engine (the MoveUnchanged
+hashes) carry state from one run to the next: pass the same AnchorFinder to
+repeated runs of one pipe, a fresh one for a new pipe.
 """
-import numpy as np
-
-from . import _capi
 from .anchor_finder import AnchorFinder
-from .blockset import BlockSetEngine
 
 
 def anchor_blocks(r):
@@ -29,35 +28,15 @@ def anchor_blocks(r):
 
 
 def block_order(b):
-    """Canonical block order before ConSeq: the sorted fragment coordinates."""
+    """Canonical block order before ConSeq: the sorted fragment coordinates
+    (the order the engine pins, for the oracle side of the tests)."""
     return sorted((f[0], f[1], f[2], f[3]) for f in b)
 
 
 def anchor_loop_fast(eng, af=None):
     """Runs AnchorLoopFast on `eng` (a BlockSetEngine over the genomes) in
-    place; returns the consensus block set's statistics (anchors found, blocks
-    mapped back)."""
+    place; returns the pipe's statistics (consensus sequences, anchors found,
+    consensus blocks, blocks mapped back, consensus loop iterations)."""
     af = af or AnchorFinder()
-    eng.apply("Filter").apply("Rest")
-    # ConSeq's sequence order feeds AnchorFinder's rank ties (equal size and
-    # name -> input index); the reference's is its std::set<Block*> pointer
-    # order, i.e. arbitrary: pinned here to the blocks sorted by fragments
-    eng.set_blocks(sorted(eng.blocks(), key=block_order))
-    cs = eng.conseq()
-    css = _capi.SeqSet(cs, [""] * len(cs))  # ConSeq names = block names (empty here)
-    # the pipe's ExtendLoopFast runs to convergence (set_max_iterations(-1),
-    # lua_lib.lua:697-699); DraftPangenome's cap of 10 does not apply here
-    cons = BlockSetEngine(css, max_iterations=-1)
-    af.clear_used()
-    anchors = anchor_blocks(af.find(css))
-    cons.set_blocks(anchors)
-    # ExtendAndAlign (lua_lib.lua:669-674), then ExtendLoopFast
-    cons.apply("DummyAligner").apply("FragmentsExtender --extend-length-portion:=0.5").apply("Align")
-    cons.apply("ExtendLoopFast")
-    loop_iterations = cons.stats()["iterations"]
-    n_cons = len(cons.blocks())
-    n_before = len(eng.blocks())
-    eng.deconseq(cons)
-    eng.apply("Align")
-    return dict(consensus_sequences=len(cs), anchors=len(anchors), cons_blocks=n_cons,
-                mapped_blocks=len(eng.blocks()) - n_before, loop_iterations=loop_iterations)
+    eng.apply("AnchorLoopFast", af=af)
+    return dict(eng.stats()["loop"])

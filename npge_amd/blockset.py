@@ -26,7 +26,7 @@ class BbStats(ctypes.Structure):
                 ("align_jobs", ctypes.c_int64), ("anchor_blocks", ctypes.c_int64),
                 ("stem_blocks", ctypes.c_int64), ("ms_align", ctypes.c_double),
                 ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 16),
-                ("counters", ctypes.c_int64 * 8)]
+                ("counters", ctypes.c_int64 * 8), ("loop", ctypes.c_int64 * 8)]
 
 STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", "align_batch",
                "stitch", "fix_ends", "overlapless_union", "blockset_hash", "filter",
@@ -35,6 +35,8 @@ STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", 
 JOB_STATS = 24  # NPGX_JOB_STATS
 COUNTER_NAMES = ["blocks_after_extend", "filter_whole", "filter_slices", "blocks_after_filter",
                  "ou_in", "ou_rejected", "hashes", "spare"]
+LOOP_NAMES = ["consensus_sequences", "anchors", "cons_blocks", "mapped_blocks", "loop_iterations",
+              "unchanged_dropped"]
 
 
 def _bind(L):
@@ -185,9 +187,10 @@ class BlockSetEngine:
     def stats(self):
         st = BbStats()
         _capi.check(_capi.lib().npgx_blockset_stats(self._h, ctypes.byref(st)))
-        d = {k: getattr(st, k) for k, _ in BbStats._fields_ if k not in ("ms_stage", "counters")}
+        d = {k: getattr(st, k) for k, _ in BbStats._fields_ if k not in ("ms_stage", "counters", "loop")}
         d["ms_stage"] = {n: round(st.ms_stage[i], 3) for i, n in enumerate(STAGE_NAMES)}
         d["counters"] = {n: int(st.counters[i]) for i, n in enumerate(COUNTER_NAMES)}
+        d["loop"] = {n: int(st.loop[i]) for i, n in enumerate(LOOP_NAMES)}
         return d
 
     def job_stats(self):

@@ -1016,9 +1016,10 @@ static constexpr int SPLIT_W = 12;       // sync word length (the reference's al
 static constexpr int SPLIT_C = 128;      // candidate words per sync state (two per lane)
 static constexpr int SPLIT_RMAX = 512;   // largest search half-width
 static constexpr int SPLIT_SPAN = 2 * SPLIT_RMAX + SPLIT_C + 1;  // word positions per row window
-static constexpr int SPLIT_HT = 2048;    // LDS hash table entries (> 1.75 x SPLIT_SPAN)
+static constexpr int SPLIT_CT = 256;     // LDS table of the candidate words
 static constexpr int SPLIT_KMAX = 128;   // segments per job at most
-static constexpr size_t SPLIT_LDS = (size_t)SPLIT_HT * 12 + (size_t)64 * SPLIT_C * 2 + SPLIT_SPAN + SPLIT_W + 80;
+static constexpr size_t SPLIT_LDS =
+    (size_t)SPLIT_CT * 8 + (size_t)SPLIT_C * 8 + (size_t)64 * SPLIT_C * 2 + SPLIT_SPAN + SPLIT_W + 80;
 
 // segment length of a job of n rows: per-column cost grows with the rows, so
 // few-row jobs take longer segments (the sync state search costs the same)
@@ -1045,159 +1046,159 @@ __device__ __forceinline__ uint32_t base2(uint32_t c) {  // A C G T -> 0..3, any
     return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
 }
 
-// Sync state t of split job s (the start of segment t+1), one wave each
+// Sync state t of split problem s (the start of segment t+1), one wave each
 // (tasks[b] = (s, t)).  Candidates: row 0's 12-mers at x0 .. x0+127, x0 the
-// fraction (t+1)/K of row 0.  Row by row, every 12-mer of the row's window
-// around the same fraction goes into an LDS hash table (tagged with the row,
-// first and last position per word) and each candidate looks itself up: it
-// survives when it occurs exactly once in every row's window.  The state is
-// the middle of the longest run of surviving consecutive candidates, W/2 into
-// its word -- inside an identical stretch of at least 12 columns, which the
-// walk crosses column by column when it is in step there.  None survives: -1
-// in every row (segment t+1 idles).
+// fraction (t+1)/K of row 0, in a small LDS hash table.  Row by row, every
+// 12-mer of the row's window around the same fraction is looked up there (a
+// rolling word per lane over a stretch of the window) and counted per
+// candidate: a candidate survives when it occurs exactly once in every row's
+// window.  The state is the middle of the longest run of surviving
+// consecutive candidates, W/2 into its word -- inside an identical stretch of
+// at least 12 columns, which the walk crosses column by column when it is in
+// step there.  None survives: -1 in every row (segment t+1 idles).
 __global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, int n_tasks, int task0) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
-    uint32_t* hkey = lds_w;                        // tag << 24 | word
-    uint32_t* hlo = hkey + SPLIT_HT;               // max of tag << 16 | (0xFFFF - first position)
-    uint32_t* hhi = hlo + SPLIT_HT;                // max of tag << 16 | last position
-    uint16_t* P = (uint16_t*)(hhi + SPLIT_HT);     // [row][candidate] window offset of its occurrence
+    uint32_t* ckey = lds_w;                        // candidate word + 1 (0: empty)
+    uint32_t* cid = ckey + SPLIT_CT;               // its candidate index
+    uint32_t* cnt = cid + SPLIT_CT;                // this row's occurrences per candidate
+    uint32_t* cpos = cnt + SPLIT_C;                // ... and the window offset of one
+    uint16_t* P = (uint16_t*)(cpos + SPLIT_C);     // [row][candidate] window offset of its occurrence
     unsigned char* ch = (unsigned char*)(P + 64 * SPLIT_C);
     if (n_tasks < 0) n_tasks = (int)min(a.sctr[SC_FIND], (unsigned int)a.cap_find);  // the sub-job pass
-    for (int b = task0 + blockIdx.x; b < n_tasks; b += gridDim.x) {
     const int lane = threadIdx.x;
-    const int2 tk = tasks[b];
-    if (tk.x < 0) continue;  // (a sub-job k_plan_subs could not split)
-    const SaSplit sp = a.splits[tk.x];
-    const SaJob job = a.jobs[sp.job];
-    const int n = job.n, t = tk.y, R = min(sp.win, SPLIT_RMAX);
-    const int span = 2 * R + SPLIT_C + 1;
-    __syncthreads();
-    for (int e = lane; e < SPLIT_HT; e += 64) {
-        hkey[e] = 0u;
-        hlo[e] = 0u;
-        hhi[e] = 0u;
-    }
     const uint32_t WM = (1u << (2 * SPLIT_W)) - 1u;
-    uint32_t cw[2] = {0u, 0u};
-    bool ok[2] = {false, false};
-    // window chars of row i, loaded one row ahead into registers
     constexpr int PER = (SPLIT_SPAN + SPLIT_W + 63) / 64;
-    unsigned char nx[PER];
-    int lo_next = 0;
-    {
-        const char* ri;
-        int li;
-        split_row(a, sp, job, 0, ri, li);
-        lo_next = (int)((int64_t)li * (t + 1) / sp.K) - R;
-#pragma unroll
-        for (int u = 0; u < PER; u++) {
-            const int q = u * 64 + lane, p = lo_next + q;
-            nx[u] = (q < span + SPLIT_W - 1 && p >= 0 && p < li) ? (unsigned char)ri[p] : 0;
-        }
-    }
-    for (int i = 0; i < n; i++) {
-        const int lo = lo_next;
+    for (int b = task0 + blockIdx.x; b < n_tasks; b += gridDim.x) {
+        const int2 tk = tasks[b];
+        if (tk.x < 0) continue;  // (a sub-job k_plan_subs could not split)
+        const SaSplit sp = a.splits[tk.x];
+        const SaJob job = a.jobs[sp.job];
+        const int n = job.n, t = tk.y, R = min(sp.win, SPLIT_RMAX);
+        const int span = 2 * R + SPLIT_C + 1;
+        const int S = (span + 63) / 64;  // window positions per lane (a contiguous stretch)
         __syncthreads();
-#pragma unroll
-        for (int u = 0; u < PER; u++) ch[u * 64 + lane] = nx[u];
-        __syncthreads();
-        if (i + 1 < n) {
+        for (int e = lane; e < SPLIT_CT; e += 64) ckey[e] = 0u;
+        uint32_t cw[2] = {0u, 0u};
+        bool ok[2] = {false, false};
+        // window chars of row i, loaded one row ahead into registers
+        unsigned char nx[PER];
+        int lo_next = 0;
+        auto load_row = [&](int i) {
             const char* ri;
             int li;
-            split_row(a, sp, job, i + 1, ri, li);
+            split_row(a, sp, job, i, ri, li);
             lo_next = (int)((int64_t)li * (t + 1) / sp.K) - R;
 #pragma unroll
             for (int u = 0; u < PER; u++) {
                 const int q = u * 64 + lane, p = lo_next + q;
                 nx[u] = (q < span + SPLIT_W - 1 && p >= 0 && p < li) ? (unsigned char)ri[p] : 0;
             }
-        }
-        const uint32_t tag = (uint32_t)i + 1u;
-        if (i == 0) {  // the candidates: row 0 at window offsets R + c
+        };
+        load_row(0);
+        for (int i = 0; i < n; i++) {
+            const int lo = lo_next;
+            __syncthreads();
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int q = R + lane + 64 * h;
-                uint32_t x = 0, bad = 0;
-                for (int j = 0; j < SPLIT_W; j++) {
-                    const uint32_t c = base2(ch[q + j]);
-                    bad |= c >> 2;
+            for (int u = 0; u < PER; u++) ch[u * 64 + lane] = nx[u];
+            for (int e = lane; e < SPLIT_C; e += 64) cnt[e] = 0u;
+            __syncthreads();
+            if (i + 1 < n) load_row(i + 1);
+            if (i == 0) {  // the candidates: row 0 at window offsets R + c, into the table
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int q = R + lane + 64 * h;
+                    uint32_t x = 0, bad = 0;
+                    for (int j = 0; j < SPLIT_W; j++) {
+                        const uint32_t c = base2(ch[q + j]);
+                        bad |= c >> 2;
+                        x = (x << 2) | (c & 3u);
+                    }
+                    cw[h] = x & WM;
+                    ok[h] = bad == 0 && lo >= 0;
+                    if (ok[h]) {
+                        const uint32_t key = cw[h] + 1u;
+                        uint32_t e = (cw[h] * 2654435761u) >> 24;
+                        while (true) {
+                            const uint32_t old = atomicCAS(&ckey[e], 0u, key);
+                            if (old == 0u) {
+                                cid[e] = (uint32_t)(lane + 64 * h);
+                                break;
+                            }
+                            if (old == key) {  // a repeated candidate word: both fail on row 0's count
+                                ok[h] = false;
+                                break;
+                            }
+                            e = (e + 1) & (SPLIT_CT - 1);
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+            // this lane's stretch of window words, rolling
+            const int q0 = lane * S, q1 = min(span, q0 + S);
+            if (q0 < q1) {
+                uint32_t x = 0;
+                int nb = 0;
+                for (int j = 0; j < SPLIT_W - 1; j++) {
+                    const uint32_t c = base2(ch[q0 + j]);
+                    nb += (int)(c >> 2);
                     x = (x << 2) | (c & 3u);
                 }
-                cw[h] = x & WM;
-                ok[h] = bad == 0 && lo >= 0;
+                for (int q = q0; q < q1; q++) {
+                    const uint32_t cin = base2(ch[q + SPLIT_W - 1]);
+                    nb += (int)(cin >> 2);
+                    x = ((x << 2) | (cin & 3u)) & WM;
+                    if (nb == 0) {
+                        uint32_t e = (x * 2654435761u) >> 24;
+                        const uint32_t key = x + 1u;
+                        while (true) {
+                            const uint32_t k = ckey[e];
+                            if (k == key) {
+                                const uint32_t c = cid[e];
+                                atomicAdd(&cnt[c], 1u);
+                                cpos[c] = (uint32_t)q;
+                                break;
+                            }
+                            if (k == 0u) break;
+                            e = (e + 1) & (SPLIT_CT - 1);
+                        }
+                    }
+                    nb -= (int)(base2(ch[q]) >> 2);  // char q leaves the next word
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int c = lane + 64 * h;
+                if (!ok[h]) continue;
+                ok[h] = cnt[c] == 1u;
+                if (ok[h]) P[i * SPLIT_C + c] = (uint16_t)cpos[c];
             }
         }
-        // every word of the window into the table
-        for (int q = lane; q < span; q += 64) {
-            uint32_t x = 0, bad = 0;
-            for (int j = 0; j < SPLIT_W; j++) {
-                const uint32_t c = base2(ch[q + j]);
-                bad |= c >> 2;
-                x = (x << 2) | (c & 3u);
+        // the longest run of surviving consecutive candidates, its middle
+        const unsigned long long m0 = ballot(ok[0]), m1 = ballot(ok[1]);
+        int best = -1, blen = 0, run = 0;
+        for (int c = 0; c < SPLIT_C; c++) {  // (wave-uniform scan of the two masks)
+            const bool o = c < 64 ? ((m0 >> c) & 1ull) : ((m1 >> (c - 64)) & 1ull);
+            run = o ? run + 1 : 0;
+            if (run > blen) {
+                blen = run;
+                best = c - (run - 1) / 2;
             }
-            if (bad) continue;
-            x &= WM;
-            const uint32_t key = (tag << 24) | x;
-            uint32_t e = (x * 2654435761u) >> (32 - 11);
-            while (true) {
-                const uint32_t k = hkey[e];
-                if (k == key) break;
-                if ((k >> 24) != tag) {  // empty for this row (stale): claim
-                    const uint32_t old = atomicCAS(&hkey[e], k, key);
-                    if (old == k || old == key) break;
-                    continue;
-                }
-                e = (e + 1) & (SPLIT_HT - 1);
-            }
-            atomicMax(&hlo[e], (tag << 16) | (0xFFFFu - (uint32_t)q));
-            atomicMax(&hhi[e], (tag << 16) | (uint32_t)q);
         }
         __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            if (!ok[h]) continue;
-            const uint32_t key = (tag << 24) | cw[h];
-            uint32_t e = (cw[h] * 2654435761u) >> (32 - 11);
-            int at = -1;
-            while (true) {
-                const uint32_t k = hkey[e];
-                if (k == key) {
-                    const uint32_t f = hlo[e], l = hhi[e];
-                    if ((f >> 16) == tag && (l >> 16) == tag && 0xFFFFu - (f & 0xFFFFu) == (l & 0xFFFFu))
-                        at = (int)(l & 0xFFFFu);
-                    break;
-                }
-                if ((k >> 24) != tag) break;
-                e = (e + 1) & (SPLIT_HT - 1);
+        int* out = a.targets + sp.tgt + (int64_t)t * n;
+        if (lane < n) {
+            int v = -1;
+            if (best >= 0) {
+                const char* ri;
+                int li;
+                split_row(a, sp, job, lane, ri, li);
+                const int lo = (int)((int64_t)li * (t + 1) / sp.K) - R;
+                v = lo + (int)P[lane * SPLIT_C + best] + SPLIT_W / 2;
             }
-            ok[h] = at >= 0;
-            if (at >= 0) P[i * SPLIT_C + lane + 64 * h] = (uint16_t)at;
+            out[lane] = v;
         }
-    }
-    // the longest run of surviving consecutive candidates, its middle
-    const unsigned long long m0 = ballot(ok[0]), m1 = ballot(ok[1]);
-    int best = -1, blen = 0, run = 0;
-    for (int c = 0; c < SPLIT_C; c++) {  // (wave-uniform scan of the two masks)
-        const bool o = c < 64 ? ((m0 >> c) & 1ull) : ((m1 >> (c - 64)) & 1ull);
-        run = o ? run + 1 : 0;
-        if (run > blen) {
-            blen = run;
-            best = c - (run - 1) / 2;
-        }
-    }
-    __syncthreads();
-    int* out = a.targets + sp.tgt + (int64_t)t * n;
-    if (lane < n) {
-        int v = -1;
-        if (best >= 0) {
-            const char* ri;
-            int li;
-            split_row(a, sp, job, lane, ri, li);
-            const int lo = (int)((int64_t)li * (t + 1) / sp.K) - R;
-            v = lo + (int)P[lane * SPLIT_C + best] + SPLIT_W / 2;
-        }
-        out[lane] = v;
-    }
     }  // tasks
 }
 
@@ -1210,30 +1211,6 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += (long long)shfl64((unsigned long long)v, threadIdx.x % 64 ^ o);
     return v;
-}
-
-// filter_reverse for a wave of a larger workgroup (no workgroup barrier):
-// row r's segment [s0, s1) gap-filtered and reversed to C + r*cstride;
-// returns this lane's row length
-__device__ int filter_reverse_wave(const WaveCtx& w, const char* src, int cap, char* C, int cstride, int s0,
-                                   int s1) {
-    int my_len = 0;
-    for (int r = 0; r < w.n; r++) {
-        const char* a = src + (size_t)r * cap;
-        char* c = C + (size_t)r * cstride;
-        int k = 0;
-        for (int base = s1 - 1; base >= s0; base -= 64) {
-            const int idx = base - w.lane;
-            const bool in = idx >= s0;
-            const char x = in ? a[idx] : '-';
-            const bool keep = in && x != '-';
-            const unsigned long long m = ballot(keep);
-            if (keep) c[k + __popcll(m & ((1ull << w.lane) - 1ull))] = x;
-            k += __popcll(m);
-        }
-        if (w.lane == r) my_len = k;
-    }
-    return my_len;
 }
 
 // exclusive prefix sum over the POST_THREADS threads of the workgroup (every
@@ -1531,7 +1508,7 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_b
                     d.job = j;
                     d.x = rg.x;
                     d.out_cap = oc;
-                    d.pad = 0;
+                    d.pad = rg.y - rg.x + 1;  // > 0: its rows are k_sub_rows' to write
                     d.out_off = off + pb - by;
                     a.subs[sn] = d;
                     jr[ri] = make_int4(rg.x, rg.y, -(sn + 1), rg.w);
@@ -1549,18 +1526,40 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_b
         }
         return;
     }
-    for (int ri = wid; ri < R; ri += POST_THREADS / 64) {
-        const int4 rg = jr[ri];
-        if (rg.z > 0) continue;
-        const SaSub d = a.subs[-rg.z - 1];
-        const int len = filter_reverse_wave(w, A, cap, C + rg.x, cap, rg.x, rg.y + 1);
-        if (w.act) ((int*)(a.pool + d.out_off))[lane] = len;
-    }
     if (tid == 0) {
         a.job_nreg[j] = R;
         a.fin[atomicAdd(&a.counters[1], 1u)] = j;
         a.job_len[j] = L0;
         a.job_status[j] = 3;
+    }
+}
+
+// The rows of the bad regions k_split_post queued (SaSub.pad = the region's
+// width): columns [x, x + width) of every row of the job's A, gap-filtered
+// and reversed into C at column x (fix_bad_regions :443-447), the lengths
+// into the sub-job's pool header; one wave per (sub-job, row)
+__global__ __launch_bounds__(256) void k_sub_rows(SaArgs a) {
+    const unsigned long long n_pairs = a.alloc[1] * 64ull;
+    const int lane = threadIdx.x & 63;
+    for (unsigned long long p = blockIdx.x * 4ull + (threadIdx.x >> 6); p < n_pairs; p += gridDim.x * 4ull) {
+        const SaSub d = a.subs[p >> 6];
+        const int r = (int)(p & 63);
+        if (d.pad <= 0) continue;
+        const SaJob job = a.jobs[d.job];
+        if (r >= job.n) continue;
+        const char* src = (const char*)(a.scratch + job.scratch) + (size_t)r * job.cap;
+        char* dst = (char*)(a.scratch + job.scratch) + (2 * (size_t)job.n + r) * job.cap + d.x;
+        int k = 0;
+        for (int base = d.x + d.pad - 1; base >= d.x; base -= 64) {
+            const int idx = base - lane;
+            const bool in = idx >= d.x;
+            const char x = in ? src[idx] : '-';
+            const bool keep = in && x != '-';
+            const unsigned long long m = ballot(keep);
+            if (keep) dst[k + __popcll(m & ((1ull << lane) - 1ull))] = x;
+            k += __popcll(m);
+        }
+        if (lane == 0) ((int*)(a.pool + d.out_off))[r] = k;
     }
 }
 
@@ -2615,6 +2614,12 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             }
             const int lds_ints = (int)std::min<int64_t>(max_rc, 32768);
             al->d_reg_dst.grow((size_t)n_reg + jobs.size());
+            if (!splits.empty()) {  // the rows of the split jobs' bad regions
+                ti = al->timer.begin("align_sub_rows", st, 0.0, 0);
+                hipLaunchKernelGGL(k_sub_rows, dim3(1024), dim3(256), 0, st, A);
+                NPGX_HIP(hipGetLastError());
+                al->timer.end(ti, st);
+            }
             if (split_subs) {  // the long sub-jobs: plan, sync states
                 ti = al->timer.begin("align_sub_split", st, 0.0, 0);
                 hipLaunchKernelGGL(k_plan_subs, dim3(256), dim3(256), 0, st, A);
@@ -2670,6 +2675,19 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 }
                 fprintf(stderr, "split job %d n=%d K=%d maxlen=%d valid_states=%d hits=%d ovf=%d chain %s\n", sp.job,
                         n, sp.K, jmax[sp.job], valid, hits, ovf, chain.c_str());
+            }
+            if (al->want_stats) {  // the slowest segments (wall clock at 100 MHz)
+                std::vector<int64_t> sw(2 * segs.size());
+                NPGX_HIP(hipMemcpy(sw.data(), al->d_seg_wall.p, sw.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<std::pair<int64_t, int>> d;
+                for (size_t q = 0; q < segs.size(); q++) d.push_back({sw[2 * q + 1] - sw[2 * q], (int)q});
+                std::sort(d.rbegin(), d.rend());
+                for (size_t q = 0; q < std::min<size_t>(5, d.size()); q++) {
+                    const int4 r = sr[(size_t)d[q].second];
+                    fprintf(stderr, "slow segment %d: %.1f us, %d cols, next %d (K %d), n %d\n", d[q].second,
+                            d[q].first / 100.0, r.y, r.x, splits[segs[(size_t)d[q].second].split].K,
+                            jobs[splits[segs[(size_t)d[q].second].split].job].n);
+                }
             }
             if (deferring) {  // sub-jobs: count and widths
                 unsigned long long al2[2];

@@ -1,6 +1,9 @@
 """Block-build driver used by bench.py and smoke(): one step = DraftPangenome on
 a device-resident genome set (AnchorFinder -> RemoveNonStem --exact ->
-DummyAligner -> ExtendLoopFast(10) -> Filter, src/algo/lua_lib.lua:1569-1621).
+DummyAligner -> ExtendLoopFast(10) -> Filter, src/algo/lua_lib.lua:1569-1621),
+optionally followed by one AnchorLoopFast (lua_lib.lua:741-758), the pipe the
+real pipeline grows blocks with where the exact stem anchors are too few
+(C4: 32 genomes at 2 % divergence).
 """
 from .anchor_finder import AnchorFinder
 from .blockset import BlockSetEngine
@@ -9,9 +12,11 @@ STAGES = ["AnchorFinder", "RemoveNonStem", "DummyAligner", "ExtendLoopFast(10)",
 
 
 class BlockBuild:
-    def __init__(self, seqset, names, seqs, seed=1, comm=None):
+    def __init__(self, seqset, names, seqs, seed=1, comm=None, anchor_loop=False):
         self.ss = seqset
         self.seed = seed
+        self.anchor_loop = anchor_loop
+        self.loop_af = AnchorFinder() if anchor_loop else None
         self.eng = BlockSetEngine(seqset)
         if comm is not None:  # one genome set sharded over the ranks of comm
             self.eng.set_comm(comm)
@@ -19,7 +24,8 @@ class BlockBuild:
         self.af.set_opt_value("bloom-seed", self.seed)
 
     def workload_name(self, config):
-        return "%s DraftPangenome: %s" % (config, " -> ".join(STAGES))
+        return "%s DraftPangenome: %s%s" % (config, " -> ".join(STAGES),
+                                            " -> AnchorLoopFast" if self.anchor_loop else "")
 
     def run(self):
         # one AnchorFinder handle (device buffers kept); its used-hash set is
@@ -27,16 +33,26 @@ class BlockBuild:
         self.af.clear_used()
         self.eng.apply("DraftPangenome", af=self.af)
         st = self.eng.stats()
+        loop = None
+        if self.anchor_loop:  # a fresh pipe each step: its AnchorFinder's used set cleared
+            draft_kt = self.eng.kernel_times()
+            self.loop_af.clear_used()
+            self.eng.apply("AnchorLoopFast", af=self.loop_af)
+            lst = self.eng.stats()
+            loop = dict(lst["loop"], ms_host=round(lst["ms_host"], 3), ms_align=round(lst["ms_align"], 3))
+            self._extra_kt = draft_kt + self.loop_af.kernel_times()
+        else:
+            self._extra_kt = []
         return {"anchor_blocks": int(st["anchor_blocks"]), "stem_blocks": int(st["stem_blocks"]),
                 "iterations": int(st["iterations"]), "aligned_residues": int(st["aligned_residues"]),
                 "align_jobs": int(st["align_jobs"]), "ms_align_wall": round(st["ms_align"], 3),
                 "ms_host_bookkeeping": round(st["ms_host"], 3), "ms_stage": st["ms_stage"],
-                "counters": st["counters"]}
+                "counters": st["counters"], "anchor_loop": loop}
 
     def kernel_times(self):
         """Per-kernel totals of the last step: name -> (ms, bytes, launches)."""
         agg = {}
-        for k in self.af.kernel_times() + self.eng.kernel_times():
+        for k in self.af.kernel_times() + self.eng.kernel_times() + getattr(self, "_extra_kt", []):
             a = agg.setdefault(k["name"], {"name": k["name"], "ms": 0.0, "bytes": 0.0, "launches": 0})
             a["ms"] += k["ms"]
             a["bytes"] += k["bytes"]

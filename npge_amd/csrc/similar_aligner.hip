@@ -1018,8 +1018,11 @@ static constexpr int SPLIT_RMAX = 512;   // largest search half-width
 static constexpr int SPLIT_SPAN = 2 * SPLIT_RMAX + SPLIT_C + 1;  // word positions per row window
 static constexpr int SPLIT_CT = 256;     // LDS table of the candidate words
 static constexpr int SPLIT_KMAX = 128;   // segments per job at most
-static constexpr size_t SPLIT_LDS =
-    (size_t)SPLIT_CT * 8 + (size_t)SPLIT_C * 8 + (size_t)64 * SPLIT_C * 2 + SPLIT_SPAN + SPLIT_W + 80;
+static constexpr int SPLIT_WAVES = 4;    // waves per sync state (rows dealt out)
+static constexpr int SPLIT_CH = ((SPLIT_SPAN + SPLIT_W + 63) / 64) * 64;  // window chars per wave
+static constexpr size_t SPLIT_LDS = (size_t)SPLIT_CT * 8 + (size_t)SPLIT_C * 4 +
+                                    (size_t)SPLIT_WAVES * SPLIT_C * 8 + (size_t)64 * SPLIT_C * 2 +
+                                    (size_t)SPLIT_WAVES * SPLIT_CH + 64;
 
 // segment length of a job of n rows: per-column cost grows with the rows, so
 // few-row jobs take longer segments (the sync state search costs the same)
@@ -1046,28 +1049,31 @@ __device__ __forceinline__ uint32_t base2(uint32_t c) {  // A C G T -> 0..3, any
     return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
 }
 
-// Sync state t of split problem s (the start of segment t+1), one wave each
-// (tasks[b] = (s, t)).  Candidates: row 0's 12-mers at x0 .. x0+127, x0 the
-// fraction (t+1)/K of row 0, in a small LDS hash table.  Row by row, every
-// 12-mer of the row's window around the same fraction is looked up there (a
-// rolling word per lane over a stretch of the window) and counted per
-// candidate: a candidate survives when it occurs exactly once in every row's
-// window.  The state is the middle of the longest run of surviving
-// consecutive candidates, W/2 into its word -- inside an identical stretch of
-// at least 12 columns, which the walk crosses column by column when it is in
-// step there.  None survives: -1 in every row (segment t+1 idles).
-__global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, int n_tasks, int task0) {
+// Sync state t of split problem s (the start of segment t+1), one workgroup
+// each (tasks[b] = (s, t)).  Candidates: row 0's 12-mers at x0 .. x0+127, x0
+// the fraction (t+1)/K of row 0, in a small LDS hash table.  The rows are
+// dealt out to the waves: every 12-mer of a row's window around the same
+// fraction is looked up there (a rolling word per lane over a stretch of the
+// window) and counted per candidate, and a candidate survives when it occurs
+// exactly once in every row's window.  The state is the middle of the longest
+// run of surviving consecutive candidates, W/2 into its word -- inside an
+// identical stretch of at least 12 columns, which the walk crosses column by
+// column when it is in step there.  None survives: -1 in every row (segment
+// t+1 idles).
+__global__ __launch_bounds__(64 * SPLIT_WAVES) void k_split_find(SaArgs a, const int2* tasks, int n_tasks,
+                                                                 int task0) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
-    uint32_t* ckey = lds_w;                        // candidate word + 1 (0: empty)
-    uint32_t* cid = ckey + SPLIT_CT;               // its candidate index
-    uint32_t* cnt = cid + SPLIT_CT;                // this row's occurrences per candidate
-    uint32_t* cpos = cnt + SPLIT_C;                // ... and the window offset of one
-    uint16_t* P = (uint16_t*)(cpos + SPLIT_C);     // [row][candidate] window offset of its occurrence
-    unsigned char* ch = (unsigned char*)(P + 64 * SPLIT_C);
+    uint32_t* ckey = lds_w;                              // candidate word + 1 (0: empty)
+    uint32_t* cid = ckey + SPLIT_CT;                     // its candidate index
+    uint32_t* cok = cid + SPLIT_CT;                      // candidate still alive
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t* cnt = cok + SPLIT_C + wid * 2 * SPLIT_C;   // this wave's row: occurrences per candidate
+    uint32_t* cpos = cnt + SPLIT_C;                      // ... and the window offset of one
+    uint16_t* P = (uint16_t*)(cok + SPLIT_C + SPLIT_WAVES * 2 * SPLIT_C);  // [row][candidate] offsets
+    unsigned char* ch = (unsigned char*)(P + 64 * SPLIT_C) + wid * SPLIT_CH;  // this wave's window
     if (n_tasks < 0) n_tasks = (int)min(a.sctr[SC_FIND], (unsigned int)a.cap_find);  // the sub-job pass
-    const int lane = threadIdx.x;
     const uint32_t WM = (1u << (2 * SPLIT_W)) - 1u;
-    constexpr int PER = (SPLIT_SPAN + SPLIT_W + 63) / 64;
+    constexpr int PER = SPLIT_CH / 64;
     for (int b = task0 + blockIdx.x; b < n_tasks; b += gridDim.x) {
         const int2 tk = tasks[b];
         if (tk.x < 0) continue;  // (a sub-job k_plan_subs could not split)
@@ -1076,64 +1082,72 @@ __global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, 
         const int n = job.n, t = tk.y, R = min(sp.win, SPLIT_RMAX);
         const int span = 2 * R + SPLIT_C + 1;
         const int S = (span + 63) / 64;  // window positions per lane (a contiguous stretch)
-        __syncthreads();
-        for (int e = lane; e < SPLIT_CT; e += 64) ckey[e] = 0u;
-        uint32_t cw[2] = {0u, 0u};
-        bool ok[2] = {false, false};
-        // window chars of row i, loaded one row ahead into registers
+        // window chars of row i into registers, then into this wave's LDS window
         unsigned char nx[PER];
-        int lo_next = 0;
-        auto load_row = [&](int i) {
+        auto load_row = [&](int i, int& lo) {
             const char* ri;
             int li;
             split_row(a, sp, job, i, ri, li);
-            lo_next = (int)((int64_t)li * (t + 1) / sp.K) - R;
+            lo = (int)((int64_t)li * (t + 1) / sp.K) - R;
 #pragma unroll
             for (int u = 0; u < PER; u++) {
-                const int q = u * 64 + lane, p = lo_next + q;
+                const int q = u * 64 + lane, p = lo + q;
                 nx[u] = (q < span + SPLIT_W - 1 && p >= 0 && p < li) ? (unsigned char)ri[p] : 0;
             }
         };
-        load_row(0);
-        for (int i = 0; i < n; i++) {
-            const int lo = lo_next;
-            __syncthreads();
+        auto stage = [&]() {
 #pragma unroll
             for (int u = 0; u < PER; u++) ch[u * 64 + lane] = nx[u];
-            for (int e = lane; e < SPLIT_C; e += 64) cnt[e] = 0u;
-            __syncthreads();
-            if (i + 1 < n) load_row(i + 1);
-            if (i == 0) {  // the candidates: row 0 at window offsets R + c, into the table
+        };
+        __syncthreads();
+        for (int e = threadIdx.x; e < SPLIT_CT; e += 64 * SPLIT_WAVES) ckey[e] = 0u;
+        __syncthreads();
+        if (wid == 0) {  // the candidates: row 0 at window offsets R + c, into the table
+            int lo0;
+            load_row(0, lo0);
+            stage();
+            wave_or_wg_sync<false>();
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int q = R + lane + 64 * h;
-                    uint32_t x = 0, bad = 0;
-                    for (int j = 0; j < SPLIT_W; j++) {
-                        const uint32_t c = base2(ch[q + j]);
-                        bad |= c >> 2;
-                        x = (x << 2) | (c & 3u);
-                    }
-                    cw[h] = x & WM;
-                    ok[h] = bad == 0 && lo >= 0;
-                    if (ok[h]) {
-                        const uint32_t key = cw[h] + 1u;
-                        uint32_t e = (cw[h] * 2654435761u) >> 24;
-                        while (true) {
-                            const uint32_t old = atomicCAS(&ckey[e], 0u, key);
-                            if (old == 0u) {
-                                cid[e] = (uint32_t)(lane + 64 * h);
-                                break;
-                            }
-                            if (old == key) {  // a repeated candidate word: both fail on row 0's count
-                                ok[h] = false;
-                                break;
-                            }
-                            e = (e + 1) & (SPLIT_CT - 1);
+            for (int h = 0; h < 2; h++) {
+                const int q = R + lane + 64 * h;
+                uint32_t x = 0, bad = 0;
+                for (int j = 0; j < SPLIT_W; j++) {
+                    const uint32_t c = base2(ch[q + j]);
+                    bad |= c >> 2;
+                    x = (x << 2) | (c & 3u);
+                }
+                x &= WM;
+                bool ok = bad == 0 && lo0 >= 0;
+                if (ok) {
+                    const uint32_t key = x + 1u;
+                    uint32_t e = (x * 2654435761u) >> 24;
+                    while (true) {
+                        const uint32_t old = atomicCAS(&ckey[e], 0u, key);
+                        if (old == 0u) {
+                            cid[e] = (uint32_t)(lane + 64 * h);
+                            break;
                         }
+                        if (old == key) {  // a repeated candidate word: both fail on row 0's count
+                            ok = false;
+                            break;
+                        }
+                        e = (e + 1) & (SPLIT_CT - 1);
                     }
                 }
-                __syncthreads();
+                cok[lane + 64 * h] = ok;
             }
+        }
+        __syncthreads();
+        int lo_next = 0;
+        if (wid < n) load_row(wid, lo_next);
+        for (int i = wid; i < n; i += SPLIT_WAVES) {
+            const int lo = lo_next;
+            wave_or_wg_sync<false>();
+            stage();
+            for (int e = lane; e < SPLIT_C; e += 64) cnt[e] = 0u;
+            wave_or_wg_sync<false>();
+            if (i + SPLIT_WAVES < n) load_row(i + SPLIT_WAVES, lo_next);
+            (void)lo;
             // this lane's stretch of window words, rolling
             const int q0 = lane * S, q1 = min(span, q0 + S);
             if (q0 < q1) {
@@ -1166,38 +1180,39 @@ __global__ __launch_bounds__(64) void k_split_find(SaArgs a, const int2* tasks, 
                     nb -= (int)(base2(ch[q]) >> 2);  // char q leaves the next word
                 }
             }
-            __syncthreads();
+            wave_or_wg_sync<false>();
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int c = lane + 64 * h;
-                if (!ok[h]) continue;
-                ok[h] = cnt[c] == 1u;
-                if (ok[h]) P[i * SPLIT_C + c] = (uint16_t)cpos[c];
-            }
-        }
-        // the longest run of surviving consecutive candidates, its middle
-        const unsigned long long m0 = ballot(ok[0]), m1 = ballot(ok[1]);
-        int best = -1, blen = 0, run = 0;
-        for (int c = 0; c < SPLIT_C; c++) {  // (wave-uniform scan of the two masks)
-            const bool o = c < 64 ? ((m0 >> c) & 1ull) : ((m1 >> (c - 64)) & 1ull);
-            run = o ? run + 1 : 0;
-            if (run > blen) {
-                blen = run;
-                best = c - (run - 1) / 2;
+                if (cnt[c] == 1u) P[i * SPLIT_C + c] = (uint16_t)cpos[c];
+                else cok[c] = 0u;
             }
         }
         __syncthreads();
-        int* out = a.targets + sp.tgt + (int64_t)t * n;
-        if (lane < n) {
-            int v = -1;
-            if (best >= 0) {
-                const char* ri;
-                int li;
-                split_row(a, sp, job, lane, ri, li);
-                const int lo = (int)((int64_t)li * (t + 1) / sp.K) - R;
-                v = lo + (int)P[lane * SPLIT_C + best] + SPLIT_W / 2;
+        if (wid == 0) {
+            // the longest run of surviving consecutive candidates, its middle
+            const unsigned long long m0 = ballot(cok[lane] != 0u), m1 = ballot(cok[lane + 64] != 0u);
+            int best = -1, blen = 0, run = 0;
+            for (int c = 0; c < SPLIT_C; c++) {  // (wave-uniform scan of the two masks)
+                const bool o = c < 64 ? ((m0 >> c) & 1ull) : ((m1 >> (c - 64)) & 1ull);
+                run = o ? run + 1 : 0;
+                if (run > blen) {
+                    blen = run;
+                    best = c - (run - 1) / 2;
+                }
             }
-            out[lane] = v;
+            int* out = a.targets + sp.tgt + (int64_t)t * n;
+            if (lane < n) {
+                int v = -1;
+                if (best >= 0) {
+                    const char* ri;
+                    int li;
+                    split_row(a, sp, job, lane, ri, li);
+                    const int lo = (int)((int64_t)li * (t + 1) / sp.K) - R;
+                    v = lo + (int)P[lane * SPLIT_C + best] + SPLIT_W / 2;
+                }
+                out[lane] = v;
+            }
         }
     }  // tasks
 }
@@ -1262,11 +1277,14 @@ __device__ int regions_block(LdsU64w* gm, int nw, int L, int wf, int min_length,
     }
     int R = 0;
     block_scan_excl(cnt, &R, scratch4);
-    const long long need = (long long)nw * 8 + (long long)R * 9 + 64;
+    // two copies of the region arrays (a round reads one, writes the other)
+    const long long need = (long long)nw * 8 + (long long)R * 17 + 64;
     if (need > area_bytes) return -1;
     LdsInt* rx = (LdsInt*)(gm + nw);
     LdsInt* rw = rx + R;  // weight | good << 31
-    unsigned char* mf = (unsigned char*)(rw + R);  // this round's merging regions
+    LdsInt* qx = rw + R;
+    LdsInt* qw = qx + R;
+    unsigned char* mf = (unsigned char*)(qw + R);  // this round's merging regions
     // starts in order: words dealt out in contiguous runs per thread
     {
         const int per = (nw + POST_THREADS - 1) / POST_THREADS;
@@ -1322,38 +1340,38 @@ __device__ int regions_block(LdsU64w* gm, int nw, int L, int wf, int min_length,
         if (any) s_any = 1;
         __syncthreads();
         if (!s_any) break;
-        // merge (merge_region :94-119) and compact, tile by tile in order
-        int dest = 0;
-        for (int t0 = 0; t0 < R; t0 += POST_THREADS) {
-            const int i = t0 + tid;
-            int keep = 0, nx = 0, nwt = 0;
-            if (i < R) {
-                const bool m = mf[i];
-                const bool rem = (i > 0 && mf[i - 1]) || (i + 1 < R && mf[i + 1]);
-                keep = !rem;
-                nx = rx[i];
-                nwt = rw[i];
-                if (m) {
-                    int wsum = nwt & WM;
-                    if (i > 0) {
-                        nx = rx[i - 1];
-                        wsum += rw[i - 1] & WM;
-                    }
-                    if (i + 1 < R) wsum += rw[i + 1] & WM;
-                    nwt = ((((unsigned)nwt >> 31) ? 0 : 1) << 31) | wsum;
+        // merge (merge_region :94-119) and compact into the other copy: every
+        // thread a contiguous run of regions, one scan for the new places
+        const int C = (R + POST_THREADS - 1) / POST_THREADS;
+        const int i0 = min(R, tid * C), i1 = min(R, i0 + C);
+        int kept = 0;
+        for (int i = i0; i < i1; i++) kept += !((i > 0 && mf[i - 1]) || (i + 1 < R && mf[i + 1]));
+        int tot = 0;
+        int at = block_scan_excl(kept, &tot, scratch4);
+        for (int i = i0; i < i1; i++) {
+            if ((i > 0 && mf[i - 1]) || (i + 1 < R && mf[i + 1])) continue;  // merged into a neighbour
+            int nx = rx[i], nwt = rw[i];
+            if (mf[i]) {
+                int wsum = nwt & WM;
+                if (i > 0) {
+                    nx = rx[i - 1];
+                    wsum += rw[i - 1] & WM;
                 }
+                if (i + 1 < R) wsum += rw[i + 1] & WM;
+                nwt = ((((unsigned)nwt >> 31) ? 0 : 1) << 31) | wsum;
             }
-            int kt = 0;
-            const int at = dest + block_scan_excl(keep, &kt, scratch4);
-            if (keep) {
-                rx[at] = nx;
-                rw[at] = nwt;
-            }
-            __syncthreads();
-            dest += kt;
+            qx[at] = nx;
+            qw[at] = nwt;
+            at++;
         }
-        R = dest;
         __syncthreads();
+        LdsInt* t = rx;
+        rx = qx;
+        qx = t;
+        t = rw;
+        rw = qw;
+        qw = t;
+        R = tot;
     }
     if (R > out_cap) return -1;
     // survivors with their identical columns (score_of before re-alignment)
@@ -2578,7 +2596,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A.ftasks = al->d_ftasks.p;
             if (n_job_find > 0) {
                 size_t tf = al->timer.begin("align_split", st, 0.0, (int64_t)n_job_find);
-                hipLaunchKernelGGL(k_split_find, dim3((unsigned)n_job_find), dim3(64), SPLIT_LDS, st, A,
+                hipLaunchKernelGGL(k_split_find, dim3((unsigned)n_job_find), dim3(64 * SPLIT_WAVES), SPLIT_LDS, st, A,
                                    al->d_ftasks.p, n_job_find, 0);
                 NPGX_HIP(hipGetLastError());
                 al->timer.end(tf, st);
@@ -2624,7 +2642,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 ti = al->timer.begin("align_sub_split", st, 0.0, 0);
                 hipLaunchKernelGGL(k_plan_subs, dim3(256), dim3(256), 0, st, A);
                 NPGX_HIP(hipGetLastError());
-                hipLaunchKernelGGL(k_split_find, dim3(2048), dim3(64), SPLIT_LDS, st, A, al->d_ftasks.p, -1,
+                hipLaunchKernelGGL(k_split_find, dim3(2048), dim3(64 * SPLIT_WAVES), SPLIT_LDS, st, A, al->d_ftasks.p, -1,
                                    n_job_find);
                 NPGX_HIP(hipGetLastError());
                 al->timer.end(ti, st);

@@ -2180,7 +2180,7 @@ struct npgx_aligner {
     // long jobs split into segments (k_split_find, run_segment): jobs of at
     // least two rows are cut every `split` columns of their longest row
     // (NPGX_ALIGN_SPLIT; 0: never)
-    int split = 512;
+    int split = 384;
     std::vector<SaSplit> h_splits;
     std::vector<SaSeg> h_segs;
     std::vector<int2> h_ftasks;

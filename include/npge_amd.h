@@ -272,6 +272,11 @@ typedef struct {
      * added, 4 the consensus ExtendLoopFast's iterations, 5 consensus blocks
      * MoveUnchanged dropped */
     int64_t loop[8];
+    /* AnchorLoopFast wall ms: 0 Filter + Rest + order, 1 ConSeq, 2 AnchorFinder
+     * on the consensus sequences, 3 MoveUnchanged + DummyAligner, 4
+     * ExtendAndAlign (FragmentsExtender + Align), 5 ExtendLoopFast, 6 DeConSeq,
+     * 7 the closing Align (the consensus pipe's stages add into ms_stage) */
+    double ms_loop[8];
 } npgx_bb_stats;
 
 void npgx_bb_default_options(npgx_bb_options* o);
@@ -325,6 +330,11 @@ int npgx_blockset_kernel_times(const npgx_blockset* b, npgx_kernel_time* out, in
 /* aligner per-job statistics of every batch of the last apply
  * (NPGX_JOB_STATS int64 per job, layout of npgx_align_job_stats) */
 int npgx_blockset_job_stats(const npgx_blockset* b, int64_t* out, int64_t cap, int64_t* n);
+/* AnchorLoopFast keeps MoveUnchanged's memory across runs on one block set
+ * (the hashes of the consensus blocks earlier runs saw, MoveUnchanged.cpp:
+ * 37-67, the lua pipe object's state, lua_lib.lua:741-758); this drops it, so
+ * the next AnchorLoopFast acts as a freshly made pipe. */
+int npgx_blockset_reset_loop(npgx_blockset* b);
 void npgx_blockset_free(npgx_blockset* b);
 
 /* ------------------------------------------------------------------ banded DP

@@ -26,7 +26,8 @@ class BbStats(ctypes.Structure):
                 ("align_jobs", ctypes.c_int64), ("anchor_blocks", ctypes.c_int64),
                 ("stem_blocks", ctypes.c_int64), ("ms_align", ctypes.c_double),
                 ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 16),
-                ("counters", ctypes.c_int64 * 8), ("loop", ctypes.c_int64 * 8)]
+                ("counters", ctypes.c_int64 * 8), ("loop", ctypes.c_int64 * 8),
+                ("ms_loop", ctypes.c_double * 8)]
 
 STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", "align_batch",
                "stitch", "fix_ends", "overlapless_union", "blockset_hash", "filter",
@@ -37,6 +38,8 @@ COUNTER_NAMES = ["blocks_after_extend", "filter_whole", "filter_slices", "blocks
                  "ou_in", "ou_rejected", "hashes", "spare"]
 LOOP_NAMES = ["consensus_sequences", "anchors", "cons_blocks", "mapped_blocks", "loop_iterations",
               "unchanged_dropped"]
+LOOP_STAGE_NAMES = ["filter_rest", "conseq", "anchor_finder", "move_unchanged_dummy", "extend_and_align",
+                    "extend_loop_fast", "deconseq", "align"]
 
 
 def _bind(L):
@@ -60,6 +63,7 @@ def _bind(L):
     L.npgx_blockset_kernel_times.argtypes = [vp, P(_capi.KernelTime), ctypes.c_int32,
                                              P(ctypes.c_int32)]
     L.npgx_blockset_job_stats.argtypes = [vp, vp, i64, P(i64)]
+    L.npgx_blockset_reset_loop.argtypes = [vp]
     L.npgx_blockset_free.argtypes = [vp]
     L.npgx_blockset_free.restype = None
     L._bb_bound = True
@@ -131,6 +135,11 @@ class BlockSetEngine:
         _capi.check(L.npgx_blockset_apply(self._h, processor.encode(), afh))
         return self
 
+    def reset_loop(self):
+        """Forget AnchorLoopFast's MoveUnchanged hashes (a fresh pipe)."""
+        _capi.check(_capi.lib().npgx_blockset_reset_loop(self._h))
+        return self
+
     def blocks(self):
         L = _capi.lib()
         nb, nf, rb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
@@ -187,10 +196,12 @@ class BlockSetEngine:
     def stats(self):
         st = BbStats()
         _capi.check(_capi.lib().npgx_blockset_stats(self._h, ctypes.byref(st)))
-        d = {k: getattr(st, k) for k, _ in BbStats._fields_ if k not in ("ms_stage", "counters", "loop")}
+        d = {k: getattr(st, k) for k, _ in BbStats._fields_
+             if k not in ("ms_stage", "counters", "loop", "ms_loop")}
         d["ms_stage"] = {n: round(st.ms_stage[i], 3) for i, n in enumerate(STAGE_NAMES)}
         d["counters"] = {n: int(st.counters[i]) for i, n in enumerate(COUNTER_NAMES)}
         d["loop"] = {n: int(st.loop[i]) for i, n in enumerate(LOOP_NAMES)}
+        d["ms_loop"] = {n: round(st.ms_loop[i], 3) for i, n in enumerate(LOOP_STAGE_NAMES)}
         return d
 
     def job_stats(self):

@@ -234,6 +234,7 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
     const unsigned long long EPM = ~((1ull << 48) - 1);
     const uint32_t tcap = 1u << tcap_log2;
     unsigned long long ep = 0;
+    uint32_t inserted = 0;  // keys this call claimed in the global table
     for (int S0 = 0; S0 < max_shift; S0 += 64) {
         const int s = S0 + lane;
         const bool valid = s < max_shift;
@@ -423,7 +424,13 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
         }
         out.shifts += last + 1;
         if (S0 + 64 >= max_shift) break;
-        // remember this chunk's words for the next chunks
+        // remember this chunk's words for the next chunks (the table is kept
+        // at most half full: a call that would pass that gives up, -1)
+        if (inserted + 64u * (uint32_t)n > (tcap >> 1)) {
+            __syncthreads();
+            out.found = -1;
+            return out;
+        }
         if (S0 == 0) {
             uint32_t ep32 = out.epoch + 1;
             if (ep32 >= 0xFFFF) {
@@ -441,16 +448,21 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
             if (!valid) continue;
             const unsigned long long key = ep | W[k * 64 + lane];
             uint32_t slot = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tcap_log2));
+            bool claimed = false;
             while (true) {
                 const unsigned long long kk =
                     __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (kk == key) break;
                 if ((kk & EPM) != ep) {
-                    if (atomicCAS(&tkeys[slot], kk, key) == kk) break;
+                    if (atomicCAS(&tkeys[slot], kk, key) == kk) {
+                        claimed = true;
+                        break;
+                    }
                     continue;
                 }
                 slot = (slot + 1) & (tcap - 1);
             }
+            inserted += (uint32_t)__popcll(ballot(claimed));
             const unsigned long long bit = 1ull << k;
             unsigned long long m = __hip_atomic_load(&tmask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             while (true) {
@@ -751,14 +763,25 @@ struct Proc {
             prof[6] += r.chunks;
             prof[7] += 1;
 #endif
-            if (r.found) my_shift = r.my_shift;
-            return r.found != 0;
+            if (r.found > 0) my_shift = r.my_shift;
+            if (r.found < 0) table_full();
+            return r.found > 0;
         }
         const int r = find_word<LdsU64, LdsU32>(my_shift, max_shift, (LdsU64*)S.lkeys, (LdsU64*)S.lmask,
                                                 (LdsU32*)S.ldone, S.ltab_log2, lepoch, 1 << (S.ltab_log2 - 1));
         if (r >= 0) return r == 1;
-        return find_word<unsigned long long, uint32_t>(my_shift, max_shift, S.tkeys, S.tmask, S.tdone,
-                                                       S.tcap_log2, epoch, 0x7fffffff) == 1;
+        const int g = find_word<unsigned long long, uint32_t>(my_shift, max_shift, S.tkeys, S.tmask, S.tdone,
+                                                              S.tcap_log2, epoch, (1 << (S.tcap_log2 - 1)) - 64);
+        if (g < 0) table_full();
+        return g == 1;
+    }
+
+    // The slot's global word table cannot take this call's words (the host
+    // sized it below the job's bound): the walk ends here and the job is
+    // reported as overflowed, to be re-run with a table of the full bound.
+    __device__ __forceinline__ void table_full() {
+        ovf = true;
+        stop = true;
     }
 
     // 1: found (my_shift set), 0: no shift works, -1: more than `limit` inserts
@@ -1005,6 +1028,7 @@ struct Proc {
         SA_T0(t3);
         const bool al = try_aligned(sh);
         SA_ACC(3, t3);
+        if (stop) return 1;  // table_full
         if (al) {
             if (!any_lane(w, sh > 0)) {  // every prefix empty: the child adds nothing
                 append_cols(P.ac);

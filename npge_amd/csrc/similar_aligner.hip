@@ -63,6 +63,7 @@ struct SaSplit {
     int32_t win;        // half-width of the sync word search window
     int32_t sub;        // -1: the job's own rows; else the job's sub-job (a bad region) of this index
     int32_t pad;
+    int64_t post;       // >= 0: byte offset of k_split_post's global work area (chains too long for LDS)
 };
 
 // split-state counters (device): the job splits are planned on the host, the
@@ -136,6 +137,7 @@ struct SaArgs {
     int32_t* qseg;
     int32_t* qsub;
     int2* ftasks;
+    unsigned char* post_area;  // k_split_post's global work areas (SaSplit.post)
     int32_t split_len;         // segment length for a job of 16 rows (0: no splitting)
     int32_t cap_splits, cap_segs;
     int64_t cap_tgt, cap_find, cap_pool;
@@ -1014,10 +1016,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // the state appends one by one.
 static constexpr int SPLIT_W = 12;       // sync word length (the reference's aligned_check is 10)
 static constexpr int SPLIT_C = 128;      // candidate words per sync state (two per lane)
-static constexpr int SPLIT_RMAX = 512;   // largest search half-width
+static constexpr int SPLIT_RMAX = 1024;  // largest search half-width
 static constexpr int SPLIT_SPAN = 2 * SPLIT_RMAX + SPLIT_C + 1;  // word positions per row window
 static constexpr int SPLIT_CT = 256;     // LDS table of the candidate words
-static constexpr int SPLIT_KMAX = 128;   // segments per job at most
+static constexpr int SPLIT_KMAX = 1024;  // segments per job at most
 static constexpr int SPLIT_WAVES = 4;    // waves per sync state (rows dealt out)
 static constexpr int SPLIT_CH = ((SPLIT_SPAN + SPLIT_W + 63) / 64) * 64;  // window chars per wave
 static constexpr size_t SPLIT_LDS = (size_t)SPLIT_CT * 8 + (size_t)SPLIT_C * 4 +
@@ -1029,6 +1031,18 @@ static constexpr size_t SPLIT_LDS = (size_t)SPLIT_CT * 8 + (size_t)SPLIT_C * 4 +
 __host__ __device__ __forceinline__ int split_len_for(int split, int n) {
     const int f = n >= 16 ? 1 : 16 / (n > 0 ? n : 1);
     return split * (f > 8 ? 8 : f);
+}
+
+// output columns of segment k of K (longest row mx, search half-width win):
+// room for a walk that misses up to about eight sync states in a row (the
+// speculation then still chains; past that its job re-runs whole), never
+// more than the suffix bound or `limit`
+__host__ __device__ __forceinline__ int seg_cap_for(int mx, int k, int K, int win, int64_t limit) {
+    const int64_t rest = mx - (int64_t)mx * k / K + win;
+    const int64_t reach = 8ll * (mx / K + 1) + 2ll * win;
+    const int64_t lim = rest < reach ? rest : reach;
+    const int64_t c = (2 * lim + 64 + 15) & ~15ll;
+    return (int)(c < limit ? c : limit);
 }
 
 // row `lane` of a split problem: the job's input row, or the gap-filtered
@@ -1261,9 +1275,11 @@ __device__ __forceinline__ int block_scan_excl(int v, int* total, int* scratch4)
 // places can become the minimum first), and two such regions are at least
 // three places apart: so every round merges all of them at once, with the
 // reference's result.  Survivors to out[] as (start, stop, good, identical
-// columns); returns their count, or -1 when the LDS area is too small or
+// columns); returns their count, or -1 when the area (LDS, or the global
+// work area of a chain too long for LDS: G, I plain pointers) is too small or
 // more than out_cap survive.
-__device__ int regions_block(LdsU64w* gm, int nw, int L, int wf, int min_length, int area_bytes, int4* out,
+template <class G, class I>
+__device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long long area_bytes, int4* out,
                              int out_cap, int* scratch4) {
     const int tid = threadIdx.x;
     // region starts: where the identical bit flips (and column 0)
@@ -1280,10 +1296,10 @@ __device__ int regions_block(LdsU64w* gm, int nw, int L, int wf, int min_length,
     // two copies of the region arrays (a round reads one, writes the other)
     const long long need = (long long)nw * 8 + (long long)R * 17 + 64;
     if (need > area_bytes) return -1;
-    LdsInt* rx = (LdsInt*)(gm + nw);
-    LdsInt* rw = rx + R;  // weight | good << 31
-    LdsInt* qx = rw + R;
-    LdsInt* qw = qx + R;
+    I* rx = (I*)(gm + nw);
+    I* rw = rx + R;  // weight | good << 31
+    I* qx = rw + R;
+    I* qw = qx + R;
     unsigned char* mf = (unsigned char*)(qw + R);  // this round's merging regions
     // starts in order: words dealt out in contiguous runs per thread
     {
@@ -1365,7 +1381,7 @@ __device__ int regions_block(LdsU64w* gm, int nw, int L, int wf, int min_length,
             at++;
         }
         __syncthreads();
-        LdsInt* t = rx;
+        I* t = rx;
         rx = qx;
         qx = t;
         t = rw;
@@ -1398,57 +1414,74 @@ __device__ int regions_block(LdsU64w* gm, int nw, int L, int wf, int min_length,
 // and queued for k_align_sub; k_fin_copy / k_align_finish assemble B and run
 // realing_end.  A chain that overflowed or does not fit marks the job for the
 // whole-job re-run (status 1).
+struct PostShared {
+    int pk[SPLIT_KMAX], pcols[SPLIT_KMAX], pdst[SPLIT_KMAX];
+    int np, L0, fail, R, scan[POST_THREADS / 64];
+};
+
+template <class G, class I>
+__device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long long area_bytes, PostShared& ps);
+
 __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_bytes) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_p[];
-    __shared__ int pk[SPLIT_KMAX], pcols[SPLIT_KMAX], pdst[SPLIT_KMAX];
-    __shared__ int s_np, s_L0, s_fail, s_R, s_scan[POST_THREADS / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    __shared__ PostShared ps;
+    const int tid = threadIdx.x;
     const SaSplit sp = a.splits[blockIdx.x];
+    const SaJob job = a.jobs[sp.job];
+    if (tid == 0) {
+        int k = 0, col = 0, np = 0, fail = 0;
+        while (k < sp.K) {
+            const int4 r = a.seg_res[sp.seg0 + k];
+            if (r.x <= k || r.z || col + r.y > job.cap) {  // (an idle segment is never on the chain)
+                fail = 1;
+                break;
+            }
+            ps.pk[np] = sp.seg0 + k;
+            ps.pcols[np] = r.y;
+            ps.pdst[np] = col;
+            np++;
+            col += r.y;
+            k = r.x;
+        }
+        ps.np = np;
+        ps.L0 = col;
+        ps.fail = fail;
+        ps.R = 0;
+    }
+    __syncthreads();
+    const int nw = (ps.L0 + 63) >> 6;
+    // the bits and region arrays in LDS, or (a chain too long for it) in the
+    // split's global work area
+    const long long need = (long long)nw * 8 + (long long)ps.L0 * 17 + 64;
+    if (!ps.fail && need > lds_bytes && sp.post >= 0 && a.post_area)
+        split_post_body<unsigned long long, int>(a, sp, (unsigned long long*)(a.post_area + sp.post),
+                                                 (long long)nw * 8 + ((long long)job.cap + 1) * 17 + 64, ps);
+    else
+        split_post_body<LdsU64w, LdsInt>(a, sp, (LdsU64w*)lds_p, lds_bytes, ps);
+}
+
+template <class G, class I>
+__device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long long area_bytes, PostShared& ps) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int j = sp.job;
     const SaJob job = a.jobs[j];
     const int n = job.n, cap = job.cap;
     char* A = (char*)(a.scratch + job.scratch);
     char* C = A + 2 * (size_t)n * cap;
-    WaveCtx w;
-    w.lane = lane;
-    w.n = n;
-    w.rowmask = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
-    w.act = lane < n;
-    if (tid == 0) {
-        int k = 0, col = 0, np = 0, fail = 0;
-        while (k < sp.K) {
-            const int4 r = a.seg_res[sp.seg0 + k];
-            if (r.x <= k || r.z || col + r.y > cap) {  // (an idle segment is never on the chain)
-                fail = 1;
-                break;
-            }
-            pk[np] = sp.seg0 + k;
-            pcols[np] = r.y;
-            pdst[np] = col;
-            np++;
-            col += r.y;
-            k = r.x;
-        }
-        s_np = np;
-        s_L0 = col;
-        s_fail = fail;
-    }
-    __syncthreads();
-    const int L0 = s_L0, nw = (L0 + 63) >> 6;
-    if (s_fail || (long long)nw * 16 > lds_bytes) {
+    const int L0 = ps.L0, nw = (L0 + 63) >> 6;
+    if (ps.fail || (long long)nw * 16 > area_bytes) {
         if (tid == 0) {
             a.job_len[j] = 0;
             a.job_status[j] = 1;
         }
         return;
     }
-    LdsU64w* gm = (LdsU64w*)lds_p;
     for (int q = tid; q < nw; q += POST_THREADS) gm[q] = 0ull;
     __syncthreads();
-    for (int p = 0; p < s_np; p++) {  // four columns per thread, rows read as dwords
-        const SaSeg g = a.segs[pk[p]];
+    for (int p = 0; p < ps.np; p++) {  // four columns per thread, rows read as dwords
+        const SaSeg g = a.segs[ps.pk[p]];
         const char* src = (const char*)(a.seg_pool + g.out);
-        const int cols = pcols[p], d0 = pdst[p];
+        const int cols = ps.pcols[p], d0 = ps.pdst[p];
         for (int c = 4 * tid; c < cols; c += 4 * POST_THREADS) {
             const int nb = min(4, cols - c);
             const uint32_t x0 = *(const uint32_t*)(src + c);  // (rows of 16-aligned length: in bounds)
@@ -1470,7 +1503,7 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_b
     }
     __syncthreads();
     int4* jr = a.job_regions + job.reg_off;
-    const int R = regions_block(gm, nw, L0, a.P.wf, a.P.min_length, lds_bytes, jr, job.reg_cap, s_scan);
+    const int R = regions_block<G, I>(gm, nw, L0, a.P.wf, a.P.min_length, area_bytes, jr, job.reg_cap, ps.scan);
     if (R < 0 || R > job.reg_cap) {
         if (tid == 0) {
             a.job_len[j] = 0;
@@ -1499,7 +1532,7 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_b
         base = (long long)bcast64((unsigned long long)base, 0);
         s0 = (long long)bcast64((unsigned long long)s0, 0);
         if (base < 0) {
-            if (lane == 0) s_R = -1;
+            if (lane == 0) ps.R = -1;
         } else {
             long long off = base;
             int sub = (int)s0;
@@ -1537,7 +1570,7 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_b
         }
     }
     __syncthreads();
-    if (s_R < 0) {  // sub-job pool full
+    if (ps.R < 0) {  // sub-job pool full
         if (tid == 0) {
             a.job_len[j] = 0;
             a.job_status[j] = 1;
@@ -1600,10 +1633,7 @@ __global__ __launch_bounds__(256) void k_plan_subs(SaArgs a) {
         bool ok = K >= 2 && mx >= 4 * SPLIT_W;
         if (ok) {
             const int win = min(SPLIT_RMAX, 64 + mx / 128);
-            auto seg_cap = [&](int k) {  // the suffix bound, at most the sub-job's own output
-                const int64_t rest = mx - (int64_t)mx * k / K + win;
-                return (int)min((int64_t)d.out_cap, (2 * rest + 64 + 15) & ~15ll);
-            };
+            auto seg_cap = [&](int k) { return seg_cap_for(mx, k, K, win, d.out_cap); };
             int64_t bytes = 0;
             for (int k = 0; k < K; k++) bytes += ((int64_t)n * seg_cap(k) + 255) & ~255ll;
             const unsigned long long p0 = atomicAdd(pool_ctr, (unsigned long long)bytes);
@@ -1625,6 +1655,7 @@ __global__ __launch_bounds__(256) void k_plan_subs(SaArgs a) {
                 sp.win = win;
                 sp.sub = (int32_t)sn;
                 sp.pad = 0;
+                sp.post = -1;
                 ((SaSplit*)a.splits)[si] = sp;
             }
             if (ok) {
@@ -2181,11 +2212,15 @@ struct npgx_aligner {
     // least two rows are cut every `split` columns of their longest row
     // (NPGX_ALIGN_SPLIT; 0: never)
     int split = 384;
+    // bytes the per-slot scratch of one launch may take (NPGX_SLOT_BUDGET_MB;
+    // default 16 GiB: allocating much more costs seconds on first use)
+    int64_t slot_budget = 0;
     std::vector<SaSplit> h_splits;
     std::vector<SaSeg> h_segs;
     std::vector<int2> h_ftasks;
     std::vector<int32_t> h_queue, h_jmax;
     DevBuf<SaSplit> d_splits;
+    DevBuf<unsigned char> d_post;  // k_split_post's global work areas
     DevBuf<SaSeg> d_segs;
     DevBuf<int2> d_ftasks;
     DevBuf<int32_t> d_targets;
@@ -2337,8 +2372,12 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         if (attempt == 1) {  // re-run overflowed jobs at the proven bound, in a second scratch
             scratch = 0;
             max_cap = 1;
+            max_n = 1;
+            max_len = 1;
             for (int32_t j : todo) {
                 SaJob& J = jobs[j];
+                max_n = std::max(max_n, J.n);
+                max_len = std::max(max_len, jmax[j]);
                 int64_t sum = 0;
                 for (int i = 0; i < J.n; i++) sum += ne_len[J.row0 + i];
                 J.cap = (int32_t)((std::max<int64_t>(sum, 1) + 15) & ~15ll);
@@ -2357,7 +2396,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         segs.clear();
         ftasks.clear();
         queue.clear();
-        int64_t n_tgt = 0, seg_bytes = 0;
+        int64_t n_tgt = 0, seg_bytes = 0, post_bytes = 0;
         if (attempt == 0 && o.aligner_type == 0 && al->split > 0) {
             for (int32_t j : todo) {
                 const SaJob& J = jobs[j];
@@ -2372,15 +2411,20 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 sp.win = std::min(SPLIT_RMAX, 64 + mx / 128);
                 sp.sub = -1;
                 sp.pad = 0;
+                sp.post = -1;
+                {  // a chain that may outgrow k_split_post's LDS: a global work area
+                    const int64_t need = (((int64_t)J.cap + 63) / 64) * 8 + 17ll * (J.cap + 1) + 64;
+                    if (need > (int64_t)POST_LDS) {
+                        sp.post = post_bytes;
+                        post_bytes += (need + 255) & ~255ll;
+                    }
+                }
                 n_tgt += (int64_t)(K - 1) * J.n;
                 for (int k = 0; k < K; k++) {
                     SaSeg g;
                     g.split = (int32_t)splits.size();
                     g.k = k;
-                    // room for the whole suffix (a walk that passes its states
-                    // without landing on one runs to the end)
-                    const int64_t rest = mx - (int64_t)mx * k / K + sp.win;
-                    g.cap = (int32_t)std::min<int64_t>(J.cap, (2 * rest + 64 + 15) & ~15ll);
+                    g.cap = seg_cap_for(mx, k, K, sp.win, J.cap);
                     g.pad = 0;
                     g.out = seg_bytes;
                     seg_bytes += ((int64_t)J.n * g.cap + 255) & ~255ll;
@@ -2405,13 +2449,33 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->d_order.grow(queue.size());
         put(al->d_order.p, queue.data(), queue.size() * 4);
         NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
-        // per-slot scratch: word table, append_aligned stack, regions
-        // SA_WAVES_PER_EU waves on each of the 4 SIMDs of the 256 CUs
-        const size_t slots = (size_t)std::max(1, std::min(nj, 256 * 4 * SA_WAVES_PER_EU));
+        // per-slot scratch: the word table (20 B an entry), the append_aligned
+        // stack (1028 B a level) and the regions of unsplit jobs (17 B a
+        // column), for SA_WAVES_PER_EU waves on each of the 4 SIMDs of the 256
+        // CUs.  The largest job's bounds set the sizes (a call inserts at most
+        // rows x (length + 1) words and nests at most length / (aligned_check
+        // + 1) deep).  When that many slots at those sizes pass the budget,
+        // attempt 0 caps the table and the stack -- a call that would need more
+        // ends its walk and marks the job overflowed (Proc::table_full, the
+        // depth check in Proc::run) -- and attempt 1 runs fewer slots at the
+        // full bounds: the giant alignments of whole-genome blocks
+        // (AnchorLoopFast at C4) then cost memory only where they run.
+        int64_t cols_need = 256;  // good_col doubles as 64 ints of scratch
+        for (int32_t q : queue)
+            if (q >= 0) cols_need = std::max<int64_t>(cols_need, (int64_t)jobs[q].cap + 1);
         uint32_t tlog = 10;
         while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
+        int depth = max_len / std::max(1, o.aligned_check + 1) + 4;
+        auto per_slot = [&](uint32_t tl, int dp) { return (20ll << tl) + 1028ll * dp + 17ll * cols_need; };
+        size_t slots = (size_t)std::max(1, std::min(nj, 256 * 4 * SA_WAVES_PER_EU));
+        const int64_t mem_budget = std::max<int64_t>(al->slot_budget, 1ll << 22);
+        if (attempt == 0)
+            while ((int64_t)slots * per_slot(tlog, depth) > mem_budget && (tlog > 16 || depth > 512)) {
+                if (tlog > 16 && (20ll << tlog) >= 1028ll * depth) tlog--;
+                else depth = std::max(512, depth / 2);
+            }
+        slots = std::max<size_t>(1, std::min<size_t>(slots, (size_t)(mem_budget / per_slot(tlog, depth))));
         const size_t tcap = (size_t)1 << tlog;
-        const int depth = max_len / std::max(1, o.aligned_check + 1) + 4;
         // Word tables: epochs only grow from launch to launch (every slot starts
         // at the last launch's highest epoch + 1), so entries left by earlier
         // launches never match, whatever the slot layout; the tables are
@@ -2431,7 +2495,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->st_len.ensure(slots * depth * 64);
         al->st_pos.ensure(slots * depth * 64);
         al->st_col.ensure(slots * depth);
-        const int slot_cols = std::max(max_cap + 1, 256);  // good_col doubles as 64 ints of scratch
+        const int slot_cols = (int)cols_need;
         al->regions.ensure(slots * (size_t)slot_cols);
         al->good_col.ensure(slots * (size_t)slot_cols);
 
@@ -2554,6 +2618,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.qsub = nullptr;
         A.ftasks = nullptr;
         A.split_len = o.aligner_type == 0 ? al->split : 0;
+        A.post_area = nullptr;
+        if (post_bytes > 0) {
+            al->d_post.grow((size_t)post_bytes);
+            A.post_area = al->d_post.p;
+        }
         A.cap_splits = A.cap_segs = 0;
         A.cap_tgt = A.cap_find = A.cap_pool = 0;
         const int n_job_splits = (int)splits.size(), n_job_find = (int)ftasks.size();
@@ -2881,6 +2950,12 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         if (dr && *dr) a->defer_rows = std::max(0, atoi(dr));
         const char* sp = getenv("NPGX_ALIGN_SPLIT");
         if (sp && *sp) a->split = std::max(0, atoi(sp));
+        const char* sb = getenv("NPGX_SLOT_BUDGET_MB");
+        if (sb && *sb) {
+            a->slot_budget = (int64_t)std::max(1, atoi(sb)) << 20;
+        } else {
+            a->slot_budget = 16ll << 30;
+        }
         if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
             delete a;
             throw Error(NPGX_ERR_HIP, "stream creation failed");

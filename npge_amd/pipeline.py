@@ -37,9 +37,11 @@ class BlockBuild:
         if self.anchor_loop:  # a fresh pipe each step: its AnchorFinder's used set cleared
             draft_kt = self.eng.kernel_times()
             self.loop_af.clear_used()
+            self.eng.reset_loop()
             self.eng.apply("AnchorLoopFast", af=self.loop_af)
             lst = self.eng.stats()
-            loop = dict(lst["loop"], ms_host=round(lst["ms_host"], 3), ms_align=round(lst["ms_align"], 3))
+            loop = dict(lst["loop"], ms_host=round(lst["ms_host"], 3), ms_align=round(lst["ms_align"], 3),
+                        ms_loop=lst["ms_loop"], ms_stage=lst["ms_stage"])
             self._extra_kt = draft_kt + self.loop_af.kernel_times()
         else:
             self._extra_kt = []

@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace orc_ga {
@@ -30,11 +31,26 @@ struct GA {
     const char* a;
     const char* b;
     int rows, cols, gr, max_errors, gp, mm;
-    std::vector<int> score, track;
+    // The reference keeps the whole (rows+1) x (cols+1) matrix; here only the
+    // diagonal band |c - r| <= gr + 1 is stored densely (every cell align()
+    // computes or limit_range() marks) and the few other cells it touches --
+    // the frame, max_errors == -1's completion run -- live in a map whose
+    // default is the matrix's initial value (BAD_VALUE, MATCH).  Same values,
+    // so 100 kb pairs fit in memory.
+    struct Cell {
+        int s = BAD_VALUE, t = MATCH;
+    };
+    std::vector<Cell> band;
+    std::unordered_map<int64_t, Cell> off;
 
-    int idx(int r, int c) const { return (r + 1) * (cols + 1) + (c + 1); }
-    int& at(int r, int c) { return score[(size_t)idx(r, c)]; }
-    int& tr(int r, int c) { return track[(size_t)idx(r, c)]; }
+    int bw() const { return 2 * gr + 3; }
+    Cell& cell(int r, int c) {
+        const int d = c - r;
+        if (d >= -(gr + 1) && d <= gr + 1) return band[(size_t)(r + 1) * bw() + (d + gr + 1)];
+        return off[(int64_t)(r + 1) * (cols + 1) + (c + 1)];
+    }
+    int& at(int r, int c) { return cell(r, c).s; }
+    int& tr(int r, int c) { return cell(r, c).t; }
     bool in(int r, int c) const { return -1 <= r && r < rows && -1 <= c && c < cols; }
     int side() const { return std::min(std::min(rows, cols) + gr, std::max(rows, cols)); }
     int max_row() const { return std::min(rows, side()) - 1; }
@@ -50,8 +66,8 @@ struct GA {
 
     // returns false where the reference throws "row and column are not last"
     bool align(int& r_row, int& r_col) {
-        score.assign((size_t)(rows + 1) * (cols + 1), BAD_VALUE);
-        track.assign(score.size(), MATCH);
+        band.assign((size_t)(rows + 1) * bw(), Cell());
+        off.clear();
         for (int r = -1; r < rows; r++)  // limit_range
             for (int o = -1; o <= 1; o += 2) {
                 const int c = r + o * (gr + 1);

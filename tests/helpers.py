@@ -46,3 +46,60 @@ def flank_jobs(blocks, seqs, portion_x1e4=5000, extend_length=100):
                 rows.append(_text(seqs[q], begin + oo * (mx - mn + 1), sh, oo))
             jobs.append(rows)
     return jobs
+
+
+def af_digest(r, used=None):
+    """Size-independent fingerprint of an AnchorFinder SoA result: per-array
+    sha256 (int64 little-endian) plus the scalar outputs, so full-size runs
+    are compared bit-exactly against committed fixtures."""
+    import hashlib
+
+    import numpy as np
+    d = {k: int(r[k]) for k in ("members", "bits", "hashes", "n_collected", "n_found_frags")}
+    d["params"] = [int(x) for x in r["params"]]
+    d["n_blocks"] = len(r["block_start"]) - 1
+    d["n_fragments"] = len(r["seq"])
+    for k in ("block_start", "seq", "min_pos", "max_pos", "ori"):
+        a = np.ascontiguousarray(np.asarray(r[k], dtype="<i8"))
+        d["sha_" + k] = hashlib.sha256(a.tobytes()).hexdigest()
+    if used is not None:
+        a = np.ascontiguousarray(np.asarray(used, dtype="<u8"))
+        d["n_used"] = len(a)
+        d["sha_used"] = hashlib.sha256(a.tobytes()).hexdigest()
+    return d
+
+
+def blocks_digest(blocks):
+    """Order-free fingerprint of a block set given as lists of
+    (seq, min, max, ori, row) tuples (BlockSetEngine.blocks() and
+    BlockSetOracle.blocks() share that form)."""
+    import hashlib
+    canon = sorted(tuple(sorted((int(q), int(a), int(b), int(o), r) for (q, a, b, o, r) in blk))
+                   for blk in blocks)
+    return {"n_blocks": len(canon), "n_fragments": sum(len(b) for b in canon),
+            "sha_blocks": hashlib.sha256(repr(canon).encode()).hexdigest()}
+
+
+def oracle_anchor_loop(o, workers=1):
+    """AnchorLoopFast (lua_lib.lua:741-758) over the oracle's processors, on
+    BlockSetOracle `o` holding the DraftPangenome result: Filter, Rest,
+    blocks in (seq, min, max, ori) order, ConSeq; on the consensus sequences
+    AnchorFinder -> DummyAligner -> FragmentsExtender
+    --extend-length-portion:=0.5 -> MetaAligner -> ExtendLoopFast to
+    convergence; DeConSeq into `o` and MetaAligner.  Returns the consensus
+    set's stats (its ExtendLoopFast iterations)."""
+    from oracle import oracle as orc
+    from npge_amd.anchor_loop import anchor_blocks, block_order
+    o.apply("Filter")
+    o.apply("Rest")
+    o.set_blocks(sorted(o.blocks(), key=block_order))
+    cs = o.conseq()
+    oc = orc.BlockSetOracle(cs, [""] * len(cs), portion_x1e4=5000, max_iterations=-1)
+    if workers > 1:
+        oc.set_workers(workers)
+    oc.set_blocks(anchor_blocks(orc.AnchorFinder().run(cs, [""] * len(cs))))
+    for op in ("DummyAligner", "FragmentsExtender", "MetaAligner", "ExtendLoopFast"):
+        oc.apply(op)
+    o.deconseq(oc)
+    o.apply("MetaAligner")
+    return oc.stats()

@@ -39,20 +39,8 @@ def test_rest_kats():
 
 
 def _oracle_loop(o):
-    from npge_amd.anchor_loop import anchor_blocks, block_order
-    o.apply("Filter")
-    o.apply("Rest")
-    o.set_blocks(sorted(o.blocks(), key=block_order))
-    cs = o.conseq()
-    # ExtendAndAlign's FragmentsExtender --extend-length-portion:=0.5, and the
-    # pipe's ExtendLoopFast to convergence (max_iterations -1)
-    oc = orc.BlockSetOracle(cs, [""] * len(cs), portion_x1e4=5000, max_iterations=-1)
-    oc.set_blocks(anchor_blocks(orc.AnchorFinder().run(cs, [""] * len(cs))))
-    for op in ("DummyAligner", "FragmentsExtender", "MetaAligner", "ExtendLoopFast"):
-        oc.apply(op)
-    o.deconseq(oc)
-    o.apply("MetaAligner")
-    return oc.stats()
+    from helpers import oracle_anchor_loop
+    return oracle_anchor_loop(o)
 
 
 @pytest.mark.parametrize("cfg", ["tiny", "small"])

@@ -111,3 +111,25 @@ def test_dp_long_properties():
                 assert (ia, ib) == (len(x), len(y))
             else:
                 assert cost == int(r["score"][i]) <= me
+
+
+@pytest.mark.parametrize("gr,me,cut", [(63, -1, False), (63, 400, True), (20, 150, True),
+                                       (5, -1, False)])
+def test_dp_c5_shaped_pairs(gr, me, cut):
+    """C5-shaped pairs (BASELINE.json configs[4]: 1 % divergence, the
+    synth.py mutation model with 1-10 nt indels, N runs) of 20-100 kb, bit-exact
+    vs the restatement, whose band storage holds pairs of this length."""
+    from npge_amd import synth
+    rng = np.random.default_rng(1000 + gr)
+    pairs = []
+    for i in range(8):
+        L = int(rng.integers(20_000, 100_001))
+        root = rng.integers(0, 4, L).astype(np.uint8)
+        x = synth.LETTERS[root].copy()
+        y = synth.LETTERS[synth._mutate(rng, root, 0.01)].copy()
+        if i % 3 == 0:
+            p0 = int(rng.integers(0, L - 600))
+            x[p0:p0 + int(rng.integers(50, 501))] = ord("N")
+        a, b = x.tobytes().decode(), y.tobytes().decode()
+        pairs.append((a, b) if i % 2 else (b, a))
+    _check(pairs, gr, me, cut)

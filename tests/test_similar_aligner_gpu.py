@@ -155,6 +155,23 @@ def test_very_long_rows(defer, rows, split, monkeypatch):
     _check(jobs)
 
 
+@pytest.mark.parametrize("budget_mb,split", [("1", "0"), ("1", "256"), ("8", "128")])
+def test_capped_slot_scratch(budget_mb, split, monkeypatch):
+    """NPGX_SLOT_BUDGET_MB: per-slot word tables and stacks capped below the
+    jobs' bounds (the sizing giant whole-genome alignments get).  Searches
+    through unrelated tails outgrow the capped table, their jobs end as
+    overflowed and re-run at the full bound on fewer slots: same result."""
+    monkeypatch.setenv("NPGX_SLOT_BUDGET_MB", budget_mb)
+    monkeypatch.setenv("NPGX_ALIGN_SPLIT", split)
+    rng = np.random.default_rng(23)
+    jobs = []
+    for _ in range(10):
+        n = int(rng.integers(2, 18))
+        L = int(rng.integers(4000, 12000))
+        jobs.append(_family(rng, n, L, 0.05, tail_unrelated=float(rng.choice([0.0, 0.5]))))
+    _check(jobs)
+
+
 @pytest.mark.parametrize("split", ["64", "256"])
 def test_split_similar_families(split, monkeypatch):
     """Long, highly similar families (the C2/C3 flank shape: the sync states

@@ -70,11 +70,16 @@ std::string to_atgcn(const char* s, int64_t len) {
 // 64 words also yield 32 N-bitmap words via pairs of lanes.
 __global__ void k_pack(const unsigned char* __restrict__ ascii, const int64_t* __restrict__ seq_word_off,
                        const int64_t* __restrict__ seq_ascii_off, const int64_t* __restrict__ seq_n_off,
-                       const int64_t* __restrict__ seq_size, const int32_t* __restrict__ word_seq,
+                       const int64_t* __restrict__ seq_size, int32_t n_seqs,
                        int64_t total_words, uint64_t* __restrict__ words, uint64_t* __restrict__ nmask) {
     int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= total_words) return;
-    int32_t r = word_seq[w];
+    int32_t r = 0, hi = n_seqs - 1;  // the sequence holding word w (word offsets ascend)
+    while (r < hi) {
+        const int32_t mid = (r + hi + 1) >> 1;
+        if (seq_word_off[mid] <= w) r = mid;
+        else hi = mid - 1;
+    }
     int64_t local = w - seq_word_off[r];           // word index within the sequence
     int64_t base0 = local * 32;
     int64_t size = seq_size[r];
@@ -197,11 +202,13 @@ int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char*
             s->n = n;
             s->names.resize(n);
             s->data.resize(n);
+            int64_t total = 0;
             for (int32_t i = 0; i < n; i++) {
                 NPGX_REQUIRE(lens[i] >= 0, NPGX_ERR_ARG, "negative sequence length");
                 s->names[i] = names && names[i] ? names[i] : "";
-                s->data[i] = to_atgcn(seqs[i], lens[i]);
+                total += lens[i];
             }
+            heavy_for((size_t)n, total, [&](size_t i) { s->data[i] = to_atgcn(seqs[i], lens[i]); });
             // rank: size desc, name asc, input index asc
             s->by_rank.resize(n);
             std::iota(s->by_rank.begin(), s->by_rank.end(), 0);
@@ -217,7 +224,6 @@ int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char*
             s->word_off.resize(n);
             s->n_off.resize(n);
             std::vector<int64_t> ascii_off(n), size_r(n);
-            std::vector<int32_t> word_seq;
             int64_t wo = 0, no = 0, ao = 0;
             for (int32_t r = 0; r < n; r++) {
                 int64_t sz = (int64_t)s->data[s->by_rank[r]].size();
@@ -230,37 +236,33 @@ int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char*
                 wo += nw;
                 no += nw / 2;
                 ao += sz;
-                word_seq.insert(word_seq.end(), (size_t)nw, r);
             }
             s->total_words = wo;
             s->total_nwords = no;
             s->words.ensure((size_t)wo);
             s->nmask.ensure((size_t)no);
             if (wo > 0) {
-                std::string ascii;
-                ascii.reserve((size_t)ao);
-                for (int32_t r = 0; r < n; r++) ascii += s->data[s->by_rank[r]];
                 DevBuf<unsigned char> d_ascii;
                 DevBuf<int64_t> d_wo, d_ao, d_no, d_sz;
-                DevBuf<int32_t> d_ws;
-                d_ascii.ensure(ascii.size());
+                d_ascii.ensure((size_t)std::max<int64_t>(ao, 1));
                 d_wo.ensure(n);
                 d_ao.ensure(n);
                 d_no.ensure(n);
                 d_sz.ensure(n);
-                d_ws.ensure(word_seq.size());
-                NPGX_HIP(hipMemcpy(d_ascii.p, ascii.data(), ascii.size(), hipMemcpyHostToDevice));
+                for (int32_t r = 0; r < n; r++) {  // every sequence straight to its place
+                    const std::string& d = s->data[s->by_rank[r]];
+                    if (!d.empty())
+                        NPGX_HIP(hipMemcpy(d_ascii.p + ascii_off[r], d.data(), d.size(), hipMemcpyHostToDevice));
+                }
                 NPGX_HIP(hipMemcpy(d_wo.p, s->word_off.data(), n * 8, hipMemcpyHostToDevice));
                 NPGX_HIP(hipMemcpy(d_ao.p, ascii_off.data(), n * 8, hipMemcpyHostToDevice));
                 NPGX_HIP(hipMemcpy(d_no.p, s->n_off.data(), n * 8, hipMemcpyHostToDevice));
                 NPGX_HIP(hipMemcpy(d_sz.p, size_r.data(), n * 8, hipMemcpyHostToDevice));
-                NPGX_HIP(hipMemcpy(d_ws.p, word_seq.data(), word_seq.size() * 4,
-                                   hipMemcpyHostToDevice));
                 NPGX_HIP(hipMemset(s->nmask.p, 0, (size_t)no * 8));
                 int threads = 256;
                 int64_t blocks = (wo + threads - 1) / threads;
                 hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(threads), 0, 0, d_ascii.p,
-                                   d_wo.p, d_ao.p, d_no.p, d_sz.p, d_ws.p, wo, s->words.p,
+                                   d_wo.p, d_ao.p, d_no.p, d_sz.p, n, wo, s->words.p,
                                    s->nmask.p);
                 NPGX_HIP(hipGetLastError());
                 NPGX_HIP(hipDeviceSynchronize());

@@ -138,6 +138,11 @@ struct SaArgs {
     int32_t* qsub;
     int2* ftasks;
     unsigned char* post_area;  // k_split_post's global work areas (SaSplit.post)
+    int4* chain;               // per job split, from its seg0: the chain (segment, columns, first column)
+    int4* chain_hdr;           // per job split: chain length, columns, failed
+    unsigned long long* chain_bits;  // per job split without a post area: identical-column bits
+    const int64_t* bits_off;   // ... their first word
+    const int32_t* part0;      // per job split: its first k_chain_copy workgroup (n_splits + 1 entries)
     int32_t split_len;         // segment length for a job of 16 rows (0: no splitting)
     int32_t cap_splits, cap_segs;
     int64_t cap_tgt, cap_find, cap_pool;
@@ -1406,16 +1411,125 @@ __device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long 
     return R;
 }
 
-// One workgroup per split job, after k_align_jobs: the chain of its segments
-// (0 -> m1 -> m2 .. -> end) copied into the job's A with the identical-column
-// bits (count_equal_cols :416-426) on the way, FindLowSimilar's regions from
-// those bits (wave 0, in LDS: make_regions + reduce_regions), and
-// fix_bad_regions deferred: every bad region gap-filtered and reversed into C
-// and queued for k_align_sub; k_fin_copy / k_align_finish assemble B and run
-// realing_end.  A chain that overflowed or does not fit marks the job for the
-// whole-job re-run (status 1).
+// After k_align_jobs, per split job: k_split_chain follows its segments'
+// chain (0 -> m1 -> m2 .. -> end), k_chain_copy copies the chain into the
+// job's A with the identical-column bits (count_equal_cols :416-426), many
+// workgroups per job, and k_split_post (one workgroup per job) derives
+// FindLowSimilar's regions from those bits (make_regions + reduce_regions, in
+// LDS, or in the split's global work area when too long) and defers
+// fix_bad_regions: every bad region is queued as a sub-job for k_align_sub
+// (its rows gap-filtered and reversed into C by k_sub_rows); k_fin_copy /
+// k_align_finish assemble B and run realing_end.  A chain that overflowed or
+// does not fit marks the job for the whole-job re-run (status 1).
+static constexpr int CHAIN_PART = 8192;  // output columns per k_chain_copy workgroup
+
+__device__ __forceinline__ unsigned long long* split_bits(const SaArgs& a, const SaSplit& sp, int s) {
+    return sp.post >= 0 ? (unsigned long long*)(a.post_area + sp.post) : a.chain_bits + a.bits_off[s];
+}
+
+// one workgroup per job split: the segment results in parallel into LDS, the
+// walk along the chain by one thread, the chain and its identical-column bit
+// words (cleared) to global memory
+__global__ __launch_bounds__(POST_THREADS) void k_split_chain(SaArgs a) {
+    __shared__ int nx[SPLIT_KMAX], nc[SPLIT_KMAX];
+    __shared__ int s_np, s_L0, s_fail;
+    const int tid = threadIdx.x, si = blockIdx.x;
+    const SaSplit sp = a.splits[si];
+    const SaJob job = a.jobs[sp.job];
+    for (int k = tid; k < sp.K; k += POST_THREADS) {
+        const int4 r = a.seg_res[sp.seg0 + k];
+        nx[k] = r.x;
+        nc[k] = r.z ? -1 : r.y;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int k = 0, col = 0, np = 0, fail = 0;
+        int4* ch = a.chain + sp.seg0;
+        while (k < sp.K) {
+            const int nxt = nx[k], cols = nc[k];
+            if (nxt <= k || cols < 0 || col + cols > job.cap) {  // (an idle segment is never on the chain)
+                fail = 1;
+                break;
+            }
+            ch[np] = make_int4(sp.seg0 + k, cols, col, 0);
+            np++;
+            col += cols;
+            k = nxt;
+        }
+        s_np = np;
+        s_L0 = col;
+        s_fail = fail;
+        a.chain_hdr[si] = make_int4(np, col, fail, 0);
+    }
+    __syncthreads();
+    if (s_fail) return;
+    unsigned long long* gb = split_bits(a, sp, si);
+    const int nw = (s_L0 + 63) >> 6;
+    for (int q = tid; q < nw; q += POST_THREADS) gb[q] = 0ull;
+}
+
+// workgroup b: output columns [c0, c0 + CHAIN_PART) of one job split's chain
+// into A, four columns per thread (rows read as dwords), the identical
+// columns' bits OR-ed into the split's bit words
+__global__ __launch_bounds__(POST_THREADS) void k_chain_copy(SaArgs a, int n_splits) {
+    const int b = blockIdx.x, tid = threadIdx.x;
+    int lo = 0, hi = n_splits - 1;  // the split whose parts hold b
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.part0[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const int si = lo;
+    const int4 hd = a.chain_hdr[si];
+    const int c0 = (b - a.part0[si]) * CHAIN_PART, c1 = min(hd.y, c0 + CHAIN_PART);
+    if (hd.z || c0 >= c1) return;
+    const SaSplit sp = a.splits[si];
+    const SaJob job = a.jobs[sp.job];
+    const int n = job.n, cap = job.cap;
+    char* A = (char*)(a.scratch + job.scratch);
+    unsigned long long* gb = split_bits(a, sp, si);
+    const int4* ch = a.chain + sp.seg0;
+    int e0 = 0, eh = hd.x - 1;  // the chain element holding column c0
+    while (e0 < eh) {
+        const int mid = (e0 + eh + 1) >> 1;
+        if (ch[mid].z <= c0) e0 = mid;
+        else eh = mid - 1;
+    }
+    for (int e = e0; e < hd.x; e++) {
+        const int4 el = ch[e];
+        const int d0 = el.z, cols = el.y;
+        if (d0 >= c1) break;
+        const SaSeg g = a.segs[el.x];
+        const char* src = (const char*)(a.seg_pool + g.out);
+        const int cs = (max(c0 - d0, 0)) & ~3, ce = min(c1 - d0, cols);
+        for (int c = cs + 4 * tid; c < ce; c += 4 * POST_THREADS) {
+            const uint32_t x0 = *(const uint32_t*)(src + c);  // (rows of 16-aligned length: in bounds)
+            uint32_t diff = 0;
+            int lo_b = 0, hi_b = min(4, ce - c);  // this part's columns only
+            if (d0 + c < c0) lo_b = c0 - (d0 + c);
+            char* d = A + d0 + c;
+            for (int q = lo_b; q < hi_b; q++) d[q] = (char)(x0 >> (8 * q));
+            for (int r = 1; r < n; r++) {
+                const uint32_t x = *(const uint32_t*)(src + (size_t)r * g.cap + c);
+                diff |= x ^ x0;
+                char* dr = A + (size_t)r * cap + d0 + c;
+                for (int q = lo_b; q < hi_b; q++) dr[q] = (char)(x >> (8 * q));
+            }
+            unsigned long long m0 = 0, m1 = 0;
+            const int col0 = d0 + c, w0 = col0 >> 6;
+            for (int q = lo_b; q < hi_b; q++)
+                if (!((diff >> (8 * q)) & 0xFFu)) {
+                    const int col = col0 + q;
+                    if ((col >> 6) == w0) m0 |= 1ull << (col & 63);
+                    else m1 |= 1ull << (col & 63);
+                }
+            if (m0) atomicOr(&gb[w0], m0);
+            if (m1) atomicOr(&gb[w0 + 1], m1);
+        }
+    }
+}
+
 struct PostShared {
-    int pk[SPLIT_KMAX], pcols[SPLIT_KMAX], pdst[SPLIT_KMAX];
     int np, L0, fail, R, scan[POST_THREADS / 64];
 };
 
@@ -1425,39 +1539,30 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
 __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_bytes) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_p[];
     __shared__ PostShared ps;
-    const int tid = threadIdx.x;
-    const SaSplit sp = a.splits[blockIdx.x];
+    const int tid = threadIdx.x, si = blockIdx.x;
+    const SaSplit sp = a.splits[si];
     const SaJob job = a.jobs[sp.job];
+    const int4 hd = a.chain_hdr[si];
     if (tid == 0) {
-        int k = 0, col = 0, np = 0, fail = 0;
-        while (k < sp.K) {
-            const int4 r = a.seg_res[sp.seg0 + k];
-            if (r.x <= k || r.z || col + r.y > job.cap) {  // (an idle segment is never on the chain)
-                fail = 1;
-                break;
-            }
-            ps.pk[np] = sp.seg0 + k;
-            ps.pcols[np] = r.y;
-            ps.pdst[np] = col;
-            np++;
-            col += r.y;
-            k = r.x;
-        }
-        ps.np = np;
-        ps.L0 = col;
-        ps.fail = fail;
+        ps.np = hd.x;
+        ps.L0 = hd.y;
+        ps.fail = hd.z;
         ps.R = 0;
     }
-    __syncthreads();
-    const int nw = (ps.L0 + 63) >> 6;
-    // the bits and region arrays in LDS, or (a chain too long for it) in the
-    // split's global work area
-    const long long need = (long long)nw * 8 + (long long)ps.L0 * 17 + 64;
-    if (!ps.fail && need > lds_bytes && sp.post >= 0 && a.post_area)
+    const int nw = (hd.y + 63) >> 6;
+    if (sp.post >= 0 && !hd.z) {  // the bits are already in the split's global work area
+        __syncthreads();
         split_post_body<unsigned long long, int>(a, sp, (unsigned long long*)(a.post_area + sp.post),
                                                  (long long)nw * 8 + ((long long)job.cap + 1) * 17 + 64, ps);
-    else
-        split_post_body<LdsU64w, LdsInt>(a, sp, (LdsU64w*)lds_p, lds_bytes, ps);
+        return;
+    }
+    LdsU64w* gm = (LdsU64w*)lds_p;
+    if (!hd.z && (long long)nw * 16 <= lds_bytes) {
+        const unsigned long long* gb = a.chain_bits + a.bits_off[si];
+        for (int q = tid; q < nw; q += POST_THREADS) gm[q] = gb[q];
+    }
+    __syncthreads();
+    split_post_body<LdsU64w, LdsInt>(a, sp, gm, lds_bytes, ps);
 }
 
 template <class G, class I>
@@ -1476,32 +1581,6 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
         }
         return;
     }
-    for (int q = tid; q < nw; q += POST_THREADS) gm[q] = 0ull;
-    __syncthreads();
-    for (int p = 0; p < ps.np; p++) {  // four columns per thread, rows read as dwords
-        const SaSeg g = a.segs[ps.pk[p]];
-        const char* src = (const char*)(a.seg_pool + g.out);
-        const int cols = ps.pcols[p], d0 = ps.pdst[p];
-        for (int c = 4 * tid; c < cols; c += 4 * POST_THREADS) {
-            const int nb = min(4, cols - c);
-            const uint32_t x0 = *(const uint32_t*)(src + c);  // (rows of 16-aligned length: in bounds)
-            uint32_t diff = 0;
-            char* d = A + d0 + c;
-            for (int b = 0; b < nb; b++) d[b] = (char)(x0 >> (8 * b));
-            for (int r = 1; r < n; r++) {
-                const uint32_t x = *(const uint32_t*)(src + (size_t)r * g.cap + c);
-                diff |= x ^ x0;
-                char* dr = A + (size_t)r * cap + d0 + c;
-                for (int b = 0; b < nb; b++) dr[b] = (char)(x >> (8 * b));
-            }
-            for (int b = 0; b < nb; b++)
-                if (!((diff >> (8 * b)) & 0xFFu)) {
-                    const int col = d0 + c + b;
-                    atomicOr((unsigned long long*)&gm[col >> 6], 1ull << (col & 63));
-                }
-        }
-    }
-    __syncthreads();
     int4* jr = a.job_regions + job.reg_off;
     const int R = regions_block<G, I>(gm, nw, L0, a.P.wf, a.P.min_length, area_bytes, jr, job.reg_cap, ps.scan);
     if (R < 0 || R > job.reg_cap) {
@@ -2221,6 +2300,12 @@ struct npgx_aligner {
     std::vector<int32_t> h_queue, h_jmax;
     DevBuf<SaSplit> d_splits;
     DevBuf<unsigned char> d_post;  // k_split_post's global work areas
+    DevBuf<int4> d_chain, d_chain_hdr;
+    DevBuf<unsigned long long> d_chain_bits;
+    DevBuf<int64_t> d_bits_off;
+    DevBuf<int32_t> d_part0;
+    std::vector<int64_t> h_bits_off;
+    std::vector<int32_t> h_part0;
     DevBuf<SaSeg> d_segs;
     DevBuf<int2> d_ftasks;
     DevBuf<int32_t> d_targets;
@@ -2396,7 +2481,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         segs.clear();
         ftasks.clear();
         queue.clear();
-        int64_t n_tgt = 0, seg_bytes = 0, post_bytes = 0;
+        int64_t n_tgt = 0, seg_bytes = 0, post_bytes = 0, bits_words = 0;
+        std::vector<int64_t>& bits_off = al->h_bits_off;
+        std::vector<int32_t>& part0 = al->h_part0;
+        bits_off.clear();
+        part0.assign(1, 0);
         if (attempt == 0 && o.aligner_type == 0 && al->split > 0) {
             for (int32_t j : todo) {
                 const SaJob& J = jobs[j];
@@ -2418,6 +2507,9 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                         sp.post = post_bytes;
                         post_bytes += (need + 255) & ~255ll;
                     }
+                    bits_off.push_back(bits_words);  // (unused with a post area)
+                    if (sp.post < 0) bits_words += J.cap / 64 + 1;
+                    part0.push_back(part0.back() + (J.cap + CHAIN_PART - 1) / CHAIN_PART);
                 }
                 n_tgt += (int64_t)(K - 1) * J.n;
                 for (int k = 0; k < K; k++) {
@@ -2623,6 +2715,25 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             al->d_post.grow((size_t)post_bytes);
             A.post_area = al->d_post.p;
         }
+        A.chain = nullptr;
+        A.chain_hdr = nullptr;
+        A.chain_bits = nullptr;
+        A.bits_off = nullptr;
+        A.part0 = nullptr;
+        if (!splits.empty()) {
+            al->d_chain.grow(segs.size());
+            al->d_chain_hdr.grow(splits.size());
+            al->d_chain_bits.grow((size_t)std::max<int64_t>(bits_words, 1));
+            al->d_bits_off.grow(bits_off.size());
+            al->d_part0.grow(part0.size());
+            put(al->d_bits_off.p, bits_off.data(), bits_off.size() * 8);
+            put(al->d_part0.p, part0.data(), part0.size() * 4);
+            A.chain = al->d_chain.p;
+            A.chain_hdr = al->d_chain_hdr.p;
+            A.chain_bits = al->d_chain_bits.p;
+            A.bits_off = al->d_bits_off.p;
+            A.part0 = al->d_part0.p;
+        }
         A.cap_splits = A.cap_segs = 0;
         A.cap_tgt = A.cap_find = A.cap_pool = 0;
         const int n_job_splits = (int)splits.size(), n_job_find = (int)ftasks.size();
@@ -2679,6 +2790,13 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
         if (!splits.empty()) {  // the split jobs: chain, regions, deferred bad regions
+            ti = al->timer.begin("align_split_chain", st, 0.0, (int64_t)splits.size());
+            hipLaunchKernelGGL(k_split_chain, dim3((unsigned)splits.size()), dim3(POST_THREADS), 0, st, A);
+            NPGX_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_chain_copy, dim3((unsigned)part0.back()), dim3(POST_THREADS), 0, st, A,
+                               (int)splits.size());
+            NPGX_HIP(hipGetLastError());
+            al->timer.end(ti, st);
             ti = al->timer.begin("align_split_post", st, 0.0, (int64_t)splits.size());
             hipLaunchKernelGGL(k_split_post, dim3((unsigned)splits.size()), dim3(POST_THREADS), POST_LDS, st, A,
                                (int)POST_LDS);

@@ -137,9 +137,13 @@ void npgx_af_free(npgx_af* af);
  * ranges, one per rank; the result equals npgx_af_run on one GPU bit for bit.
  * The exchange steps go through caller-supplied collectives (the host binds
  * them to torch.distributed -- RCCL over xGMI on MI355X, gloo in tests):
- *   1. the Bloom first-setter array: element-wise MIN over ranks (the
+ *   1. the Bloom bit arrays (m / 8 bytes per rank): all-gather; each rank
+ *      ORs the lower ranks' arrays, whose windows all precede its own, and
+ *      tests its windows against that OR and its own first-setter orders (the
  *      reference's sequential "bits set by an earlier window", BloomFilter.cpp
- *      :65-76, AnchorFinder.cpp:170-197, is a MIN of window orders per bit);
+ *      :65-76, AnchorFinder.cpp:170-197); then every rank's last window
+ *      (order, found): all-gather of one value (the `similar` rule across a
+ *      rank boundary, :185-192);
  *   2. the collected hashes (bloomtg_postprocess :213-218): all-gather;
  *   3. FoundFragment counts per hash (truncation :356-391): SUM;
  *   4. the FoundFragment keys of the kept groups: all-gather.

@@ -251,11 +251,32 @@ __global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __rest
 
 // found/collect of one epoch, reading P (bits of the earlier epochs) and
 // adding this epoch's bits to Pn (copied to P before the next epoch)
+// Sharded mode (bound != null): P holds the bits set by the lower ranks'
+// windows and first[] the orders of this rank's own, so the exact test of a
+// window of this range uses both; the range's first window, whose predecessor
+// lies on another rank, is not collected here but reported in bound[0..1]
+// (found, hash) and the found state of the range's last window in bound[2]:
+// the host settles the boundary after one small exchange.
+__device__ __forceinline__ bool found_at_p(const AfArgs& a, const SeqMeta& s, int64_t p,
+                                           const uint32_t* __restrict__ first, const uint32_t* __restrict__ P,
+                                           uint64_t& h) {
+    uint64_t dir;
+    if (!admitted(a, s, p, h, dir)) return false;
+    const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
+    bool f = true;
+    for (int i = 0; i < a.kb; i++) {
+        const uint32_t idx = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+        f &= bit_in(P, idx) || first[idx] < ord;
+    }
+    return f;
+}
+
 __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t* __restrict__ first,
                                                         const uint32_t* __restrict__ P,
                                                         uint32_t* __restrict__ Pn,
                                                         uint64_t* __restrict__ out,
-                                                        unsigned long long* __restrict__ n_out) {
+                                                        unsigned long long* __restrict__ n_out,
+                                                        unsigned long long* __restrict__ bound) {
     __shared__ uint8_t fs[WG];
     const Chunk c = a.chunks[blockIdx.x];
     const SeqMeta s = a.meta[c.seq];
@@ -304,15 +325,29 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
     fs[t] = f;
     __syncthreads();
     bool prev;
+    bool col;
     if (t > 0) {
         prev = fs[t - 1];
-    } else {
+        col = f && !(a.similar && prev);
+    } else if (!bound) {
         // p-1 may belong to an earlier epoch (P then holds bits set after it):
         // the exact test on first[] alone
         uint64_t hp;
         prev = found_at(a, s, p - 1, first, hp);
+        col = f && !(a.similar && prev);
+    } else if (blockIdx.x == 0 && p > 0) {  // the predecessor is on another rank
+        bound[0] = f ? 1ull : 0ull;
+        bound[1] = h;
+        col = false;
+    } else {
+        uint64_t hp;
+        prev = found_at_p(a, s, p - 1, first, P, hp);
+        col = f && !(a.similar && prev);
     }
-    const bool col = f && !(a.similar && prev);
+    if (bound && blockIdx.x == gridDim.x - 1) {  // the range's last window
+        const int64_t last = min((int64_t)WG, s.size - a.k + 1 - c.pos) - 1;
+        if (t == last) bound[2] = f ? 1ull : 0ull;
+    }
     const unsigned long long mask = __ballot(col);
     if (mask == 0) return;
     const int lane = t & 63;
@@ -324,6 +359,24 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
         const unsigned long long below = mask & ((1ull << lane) - 1ull);
         out[base + __popcll(below)] = h;
     }
+}
+
+// this rank's Bloom bits: bit b set iff a window of this rank set it
+__global__ void k_first_bits(const uint32_t* __restrict__ first, int64_t m, unsigned long long* __restrict__ bits) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool set = b < m && first[b] != 0xFFFFFFFFu;
+    const unsigned long long v = __ballot(set);  // 64 consecutive bits per wave
+    if ((threadIdx.x & 63) == 0 && b < m) bits[b >> 6] = v;
+}
+
+// P = OR of the bit arrays of the ranks below `rank` (gathered in rank order)
+__global__ void k_prefix_or(const unsigned long long* __restrict__ g, int64_t words, int rank,
+                            unsigned long long* __restrict__ P) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= words) return;
+    unsigned long long v = 0;
+    for (int q = 0; q < rank; q++) v |= g[(int64_t)q * words + w];
+    P[w] = v;
 }
 
 __global__ void k_table_insert(const uint64_t* __restrict__ hs, int64_t n, uint64_t* keys,
@@ -649,9 +702,9 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
 
     // --- pass 1: Bloom first-setter + found/collect
     af->first.ensure((size_t)m);
-    af->counters.ensure(4);
+    af->counters.ensure(8);  // [0] collected, [1] unique, [4..6] sharded boundary
     NPGX_HIP(hipMemsetAsync(af->counters.p, 0, 4 * sizeof(unsigned long long), st));
-    af->hraw.ensure((size_t)std::max<int64_t>(local_windows, 1));
+    af->hraw.ensure((size_t)local_windows + 1);
     size_t ti = 0;
     if (!comm && af->opt.bloom_epochs != 1) {
         // epochs of consecutive chunks (SeqMeta order); bits set by earlier
@@ -677,7 +730,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
             ti = af->timer.begin("found_collect", st, n_windows * (0.375 + 4.0 * kb) * double(ne) / nchunks, 0);
             const bool more = e0 + ne < nchunks;
             hipLaunchKernelGGL(k_found_collect_f, eg, block, 0, st, E, af->first.p, af->bloom_bits.p,
-                               more ? af->bloom_bits.p + words : nullptr, af->hraw.p, af->counters.p);
+                               more ? af->bloom_bits.p + words : nullptr, af->hraw.p, af->counters.p, nullptr);
             NPGX_HIP(hipGetLastError());
             af->timer.end(ti, st);
             if (more)
@@ -690,25 +743,78 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     if (run_local) hipLaunchKernelGGL(k_bloom_first, grid, block, 0, st, A, af->first.p);
     NPGX_HIP(hipGetLastError());
     af->timer.end(ti, st);
-    if (comm) {
-        // exchange 1: first[bit] = MIN over ranks (windows of every rank)
-        const dim3 fg((unsigned)((m + 255) / 256));
-        ti = af->timer.begin("first_allreduce", st, (double)m * 4 * 2, m);
-        hipLaunchKernelGGL(k_flip_sign, fg, dim3(256), 0, st, af->first.p, (int64_t)m);
-        NPGX_HIP(stream_wait(st));
-        comm_check(comm->allreduce_i32(comm->user, (int32_t*)af->first.p, m, NPGX_OP_MIN),
-                   "allreduce(first, MIN)");
-        hipLaunchKernelGGL(k_flip_sign, fg, dim3(256), 0, st, af->first.p, (int64_t)m);
+    if (!comm) {
+        ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
+        if (run_local)
+            hipLaunchKernelGGL(k_found_collect, grid, block, 0, st, A, af->first.p, af->hraw.p,
+                               af->counters.p);
         NPGX_HIP(hipGetLastError());
         af->timer.end(ti, st);
+    } else {
+        // exchange 1: every rank's Bloom bit array (m / 8 bytes, not the m
+        // first-setter orders); this rank keeps the OR of the lower ranks',
+        // whose windows all precede its own: a window here is found iff each
+        // of its bits is in that OR or was set by an earlier window of this
+        // rank (first[], local) -- the reference's sequential test exactly
+        const int64_t words = ((int64_t)m + 63) / 64;
+        af->bloom_bits.ensure((size_t)(4 * words));  // this rank's bits | P (uint64 words)
+        unsigned long long* mine = (unsigned long long*)af->bloom_bits.p;
+        unsigned long long* P = mine + words;
+        ti = af->timer.begin("bloom_bits_exchange", st, (double)m / 8 * world, m);
+        hipLaunchKernelGGL(k_first_bits, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, af->first.p,
+                           (int64_t)m, mine);
+        NPGX_HIP(hipGetLastError());
+        std::vector<int64_t> cnt(world, words);
+        af->gathered.grow((size_t)(words * world));
+        NPGX_HIP(stream_wait(st));
+        comm_check(comm->allgatherv_u64(comm->user, (const uint64_t*)mine, cnt.data(), af->gathered.p),
+                   "allgatherv(Bloom bits)");
+        hipLaunchKernelGGL(k_prefix_or, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st,
+                           (const unsigned long long*)af->gathered.p, words, rank, P);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
+        // found/collect over this rank's range; its first window's
+        // predecessor lies on a lower rank: settled after exchange 2
+        NPGX_HIP(hipMemsetAsync(af->counters.p + 4, 0, 3 * 8, st));
+        ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
+        if (run_local)
+            hipLaunchKernelGGL(k_found_collect_f, grid, block, 0, st, A, af->first.p, (const uint32_t*)P,
+                               nullptr, af->hraw.p, af->counters.p, af->counters.p + 4);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
+        NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8 * 8, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(stream_wait(st));
+        // exchange 2: every rank's last window (order, found)
+        int64_t mine_last = -1;
+        uint64_t first_order = 0;
+        bool pred_elsewhere = false;
+        if (run_local) {
+            const Chunk& cf = chunks[c0];
+            const Chunk& cl = chunks[c1 - 1];
+            const int64_t last_p = std::min<int64_t>(WG, meta[cl.seq].size - k + 1 - cl.pos) - 1 + cl.pos;
+            mine_last = (int64_t)(((meta[cl.seq].order_off + (uint64_t)last_p) << 1) | (hp[6] & 1ull));
+            first_order = meta[cf.seq].order_off + (uint64_t)cf.pos;
+            pred_elsewhere = cf.pos > 0;
+        }
+        std::vector<int64_t> lasts(world);
+        comm_check(comm->allgather_i64(comm->user, mine_last, lasts.data()), "allgather(boundary windows)");
+        if (pred_elsewhere && (hp[4] & 1ull)) {
+            bool prev = false, seen = false;
+            for (int q = 0; q < world; q++)
+                if (lasts[q] >= 0 && (uint64_t)(lasts[q] >> 1) + 1 == first_order) {
+                    prev = (lasts[q] & 1) != 0;
+                    seen = true;
+                }
+            NPGX_REQUIRE(seen, NPGX_ERR_STATE, "sharded run: the boundary window's rank is missing");
+            if (!(af->opt.anchor_similar && prev)) {  // collected after all: appended
+                const uint64_t h0 = hp[5];
+                const uint64_t n1 = hp[0] + 1;
+                NPGX_HIP(hipMemcpyAsync(af->hraw.p + hp[0], &h0, 8, hipMemcpyHostToDevice, st));
+                NPGX_HIP(hipMemcpyAsync(af->counters.p, &n1, 8, hipMemcpyHostToDevice, st));
+                NPGX_HIP(stream_wait(st));
+            }
+        }
     }
-
-    ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
-    if (run_local)
-        hipLaunchKernelGGL(k_found_collect, grid, block, 0, st, A, af->first.p, af->hraw.p,
-                           af->counters.p);
-    NPGX_HIP(hipGetLastError());
-    af->timer.end(ti, st);
     }
     NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8, hipMemcpyDeviceToHost, st));
     NPGX_HIP(stream_wait(st));

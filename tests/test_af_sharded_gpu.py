@@ -72,6 +72,9 @@ def _worker(rank, world, port, config, maxf, similar, staging, out):
     (3, "small", 5000, True, "cpu"),
     (2, "tiny", 100000, False, "cpu"),
     (2, "small", 100000, True, "cuda"),   # device staging tensors (the RCCL adapter's path)
+    (4, "small", 100000, True, "cpu"),    # rank boundaries inside sequences: the `similar` rule across ranks
+    (5, "tiny", 100000, True, "cpu"),
+    (4, "tiny", 100000, False, "cpu"),
 ])
 def test_sharded_equals_single(world, config, maxf, similar, staging):
     mgr = mp.Manager()

@@ -251,12 +251,13 @@ __global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __rest
 
 // found/collect of one epoch, reading P (bits of the earlier epochs) and
 // adding this epoch's bits to Pn (copied to P before the next epoch)
-// Sharded mode (bound != null): P holds the bits set by the lower ranks'
-// windows and first[] the orders of this rank's own, so the exact test of a
-// window of this range uses both; the range's first window, whose predecessor
-// lies on another rank, is not collected here but reported in bound[0..1]
-// (found, hash) and the found state of the range's last window in bound[2]:
-// the host settles the boundary after one small exchange.
+// Sharded mode (P0 != null): P0 holds the bits set by the lower ranks'
+// windows and first[] the orders of this rank's own (for the bits outside
+// P0), so the exact test of a window of this range uses both; the range's
+// first window, whose predecessor lies on another rank, is not collected here
+// but reported in bfirst[0..1] (found, hash), and the found state of the
+// range's last window goes to blast[0]: the host settles the boundary after
+// one small exchange.
 __device__ __forceinline__ bool found_at_p(const AfArgs& a, const SeqMeta& s, int64_t p,
                                            const uint32_t* __restrict__ first, const uint32_t* __restrict__ P,
                                            uint64_t& h) {
@@ -276,7 +277,9 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
                                                         uint32_t* __restrict__ Pn,
                                                         uint64_t* __restrict__ out,
                                                         unsigned long long* __restrict__ n_out,
-                                                        unsigned long long* __restrict__ bound) {
+                                                        const uint32_t* __restrict__ P0,
+                                                        unsigned long long* __restrict__ bfirst,
+                                                        unsigned long long* __restrict__ blast) {
     __shared__ uint8_t fs[WG];
     const Chunk c = a.chunks[blockIdx.x];
     const SeqMeta s = a.meta[c.seq];
@@ -329,24 +332,24 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
     if (t > 0) {
         prev = fs[t - 1];
         col = f && !(a.similar && prev);
-    } else if (!bound) {
+    } else if (!P0) {
         // p-1 may belong to an earlier epoch (P then holds bits set after it):
         // the exact test on first[] alone
         uint64_t hp;
         prev = found_at(a, s, p - 1, first, hp);
         col = f && !(a.similar && prev);
-    } else if (blockIdx.x == 0 && p > 0) {  // the predecessor is on another rank
-        bound[0] = f ? 1ull : 0ull;
-        bound[1] = h;
+    } else if (bfirst && blockIdx.x == 0 && p > 0) {  // the predecessor is on another rank
+        bfirst[0] = f ? 1ull : 0ull;
+        bfirst[1] = h;
         col = false;
     } else {
         uint64_t hp;
-        prev = found_at_p(a, s, p - 1, first, P, hp);
+        prev = found_at_p(a, s, p - 1, first, P0, hp);
         col = f && !(a.similar && prev);
     }
-    if (bound && blockIdx.x == gridDim.x - 1) {  // the range's last window
+    if (blast && blockIdx.x == gridDim.x - 1) {  // the range's last window
         const int64_t last = min((int64_t)WG, s.size - a.k + 1 - c.pos) - 1;
-        if (t == last) bound[2] = f ? 1ull : 0ull;
+        if (t == last) blast[0] = f ? 1ull : 0ull;
     }
     const unsigned long long mask = __ballot(col);
     if (mask == 0) return;
@@ -361,12 +364,18 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
     }
 }
 
-// this rank's Bloom bits: bit b set iff a window of this rank set it
-__global__ void k_first_bits(const uint32_t* __restrict__ first, int64_t m, unsigned long long* __restrict__ bits) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool set = b < m && first[b] != 0xFFFFFFFFu;
-    const unsigned long long v = __ballot(set);  // 64 consecutive bits per wave
-    if ((threadIdx.x & 63) == 0 && b < m) bits[b >> 6] = v;
+// this rank's Bloom bit array: the bits its admitted windows set
+__global__ __launch_bounds__(WG) void k_bloom_bits(AfArgs a, uint32_t* __restrict__ bits) {
+    const Chunk c = a.chunks[blockIdx.x];
+    const SeqMeta s = a.meta[c.seq];
+    const int64_t p = c.pos + threadIdx.x;
+    uint64_t h, dir;
+    if (!admitted(a, s, p, h, dir)) return;
+    for (int i = 0; i < a.kb; i++) {
+        const uint32_t idx = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+        const uint32_t bit = 1u << (idx & 31);
+        if (!(bits[idx >> 5] & bit)) atomicOr(&bits[idx >> 5], bit);
+    }
 }
 
 // P = OR of the bit arrays of the ranks below `rank` (gathered in rank order)
@@ -706,85 +715,85 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     NPGX_HIP(hipMemsetAsync(af->counters.p, 0, 4 * sizeof(unsigned long long), st));
     af->hraw.ensure((size_t)local_windows + 1);
     size_t ti = 0;
-    if (!comm && af->opt.bloom_epochs != 1) {
+    // bit arrays (uint32 words, W each): P (bits set before this epoch) | Pn
+    // (through this one) | this rank's bits | P0 (the lower ranks' bits)
+    const int64_t w64 = ((int64_t)m + 63) / 64, W = 2 * w64;
+    af->bloom_bits.ensure((size_t)(4 * W));
+    uint32_t* P = af->bloom_bits.p;
+    uint32_t* Pn = P + W;
+    uint32_t* mine = P + 2 * W;
+    uint32_t* P0 = nullptr;
+    unsigned long long* bfirst = comm ? af->counters.p + 4 : nullptr;
+    unsigned long long* blast = comm ? af->counters.p + 6 : nullptr;
+    ti = af->timer.begin("bloom_first", st, local_windows * (0.375 + 8.0 * kb), local_windows);
+    NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
+    if (comm) NPGX_HIP(hipMemsetAsync(af->counters.p + 4, 0, 3 * 8, st));
+    af->timer.end(ti, st);
+    if (comm) {
+        // exchange 1: every rank's Bloom bit array (m / 8 bytes); this rank
+        // keeps the OR of the lower ranks' (P0), whose windows all precede
+        // its own: a window here is found iff each of its bits is in P0 or was
+        // set by an earlier window of this rank (first[] over the bits outside
+        // P0) -- the reference's sequential test exactly.  P and Pn start at P0.
+        P0 = P + 3 * W;
+        ti = af->timer.begin("bloom_bits_exchange", st, (double)m / 8 * world, m);
+        NPGX_HIP(hipMemsetAsync(mine, 0, (size_t)W * 4, st));
+        if (run_local) hipLaunchKernelGGL(k_bloom_bits, grid, block, 0, st, A, mine);
+        NPGX_HIP(hipGetLastError());
+        std::vector<int64_t> cnt(world, w64);
+        af->gathered.grow((size_t)(w64 * world));
+        NPGX_HIP(stream_wait(st));
+        comm_check(comm->allgatherv_u64(comm->user, (const uint64_t*)mine, cnt.data(), af->gathered.p),
+                   "allgatherv(Bloom bits)");
+        hipLaunchKernelGGL(k_prefix_or, dim3((unsigned)((w64 + 255) / 256)), dim3(256), 0, st,
+                           (const unsigned long long*)af->gathered.p, w64, rank, (unsigned long long*)P0);
+        NPGX_HIP(hipGetLastError());
+        NPGX_HIP(hipMemcpyAsync(P, P0, (size_t)W * 4, hipMemcpyDeviceToDevice, st));
+        NPGX_HIP(hipMemcpyAsync(Pn, P0, (size_t)W * 4, hipMemcpyDeviceToDevice, st));
+        af->timer.end(ti, st);
+    } else {
+        NPGX_HIP(hipMemsetAsync(P, 0, (size_t)(2 * W) * 4, st));
+    }
+    if (af->opt.bloom_epochs != 1 && run_local) {
         // epochs of consecutive chunks (SeqMeta order); bits set by earlier
-        // epochs skip the atomics and the first[] reads
+        // epochs (or lower ranks) skip the atomics and the first[] reads
         const int64_t per = std::max<int64_t>(1, (int64_t)std::ceil(double(nchunks) / std::max(1, af->opt.bloom_epochs > 0
                                                                          ? af->opt.bloom_epochs
-                                                                         : (int)std::max<int64_t>(1, n_windows / (2 << 20)))));
-        const size_t words = ((size_t)m + 31) / 32;
-        af->bloom_bits.ensure(2 * words);  // P (earlier epochs) | Pn (through this one)
-        ti = af->timer.begin("bloom_first", st, n_windows * (0.375 + 8.0 * kb), n_windows);
-        NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
-        NPGX_HIP(hipMemsetAsync(af->bloom_bits.p, 0, 2 * words * 4, st));
-        af->timer.end(ti, st);
+                                                                         : (int)std::max<int64_t>(1, local_windows / (2 << 20)))));
         for (int64_t e0 = 0; e0 < nchunks; e0 += per) {
             const int64_t ne = std::min(per, nchunks - e0);
             AfArgs E = A;
             E.chunks = A.chunks + e0;
             const dim3 eg((unsigned)ne);
             ti = af->timer.begin("bloom_first", st, 0.0, 0);
-            hipLaunchKernelGGL(k_bloom_first_f, eg, block, 0, st, E, af->first.p, af->bloom_bits.p);
+            hipLaunchKernelGGL(k_bloom_first_f, eg, block, 0, st, E, af->first.p, P);
             NPGX_HIP(hipGetLastError());
             af->timer.end(ti, st);
-            ti = af->timer.begin("found_collect", st, n_windows * (0.375 + 4.0 * kb) * double(ne) / nchunks, 0);
+            ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb) * double(ne) / nchunks, 0);
             const bool more = e0 + ne < nchunks;
-            hipLaunchKernelGGL(k_found_collect_f, eg, block, 0, st, E, af->first.p, af->bloom_bits.p,
-                               more ? af->bloom_bits.p + words : nullptr, af->hraw.p, af->counters.p, nullptr);
+            hipLaunchKernelGGL(k_found_collect_f, eg, block, 0, st, E, af->first.p, P, more ? Pn : nullptr,
+                               af->hraw.p, af->counters.p, P0, e0 == 0 ? bfirst : nullptr,
+                               more ? nullptr : blast);
             NPGX_HIP(hipGetLastError());
             af->timer.end(ti, st);
-            if (more)
-                NPGX_HIP(hipMemcpyAsync(af->bloom_bits.p, af->bloom_bits.p + words, words * 4,
-                                        hipMemcpyDeviceToDevice, st));
+            if (more) NPGX_HIP(hipMemcpyAsync(P, Pn, (size_t)W * 4, hipMemcpyDeviceToDevice, st));
         }
-    } else {
-    ti = af->timer.begin("bloom_first", st, local_windows * (0.375 + 8.0 * kb), local_windows);
-    NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
-    if (run_local) hipLaunchKernelGGL(k_bloom_first, grid, block, 0, st, A, af->first.p);
-    NPGX_HIP(hipGetLastError());
-    af->timer.end(ti, st);
-    if (!comm) {
+    } else if (run_local) {
+        ti = af->timer.begin("bloom_first", st, 0.0, 0);
+        hipLaunchKernelGGL(k_bloom_first_f, grid, block, 0, st, A, af->first.p, P);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
         ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
-        if (run_local)
-            hipLaunchKernelGGL(k_found_collect, grid, block, 0, st, A, af->first.p, af->hraw.p,
-                               af->counters.p);
+        hipLaunchKernelGGL(k_found_collect_f, grid, block, 0, st, A, af->first.p, P, nullptr, af->hraw.p,
+                           af->counters.p, P0, bfirst, blast);
         NPGX_HIP(hipGetLastError());
         af->timer.end(ti, st);
-    } else {
-        // exchange 1: every rank's Bloom bit array (m / 8 bytes, not the m
-        // first-setter orders); this rank keeps the OR of the lower ranks',
-        // whose windows all precede its own: a window here is found iff each
-        // of its bits is in that OR or was set by an earlier window of this
-        // rank (first[], local) -- the reference's sequential test exactly
-        const int64_t words = ((int64_t)m + 63) / 64;
-        af->bloom_bits.ensure((size_t)(4 * words));  // this rank's bits | P (uint64 words)
-        unsigned long long* mine = (unsigned long long*)af->bloom_bits.p;
-        unsigned long long* P = mine + words;
-        ti = af->timer.begin("bloom_bits_exchange", st, (double)m / 8 * world, m);
-        hipLaunchKernelGGL(k_first_bits, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, af->first.p,
-                           (int64_t)m, mine);
-        NPGX_HIP(hipGetLastError());
-        std::vector<int64_t> cnt(world, words);
-        af->gathered.grow((size_t)(words * world));
-        NPGX_HIP(stream_wait(st));
-        comm_check(comm->allgatherv_u64(comm->user, (const uint64_t*)mine, cnt.data(), af->gathered.p),
-                   "allgatherv(Bloom bits)");
-        hipLaunchKernelGGL(k_prefix_or, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st,
-                           (const unsigned long long*)af->gathered.p, words, rank, P);
-        NPGX_HIP(hipGetLastError());
-        af->timer.end(ti, st);
-        // found/collect over this rank's range; its first window's
-        // predecessor lies on a lower rank: settled after exchange 2
-        NPGX_HIP(hipMemsetAsync(af->counters.p + 4, 0, 3 * 8, st));
-        ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
-        if (run_local)
-            hipLaunchKernelGGL(k_found_collect_f, grid, block, 0, st, A, af->first.p, (const uint32_t*)P,
-                               nullptr, af->hraw.p, af->counters.p, af->counters.p + 4);
-        NPGX_HIP(hipGetLastError());
-        af->timer.end(ti, st);
+    }
+    if (comm) {
         NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8 * 8, hipMemcpyDeviceToHost, st));
         NPGX_HIP(stream_wait(st));
-        // exchange 2: every rank's last window (order, found)
+        // exchange 2: every rank's last window (order, found): the similar
+        // rule (AnchorFinder.cpp:185-192) for this range's first window
         int64_t mine_last = -1;
         uint64_t first_order = 0;
         bool pred_elsewhere = false;
@@ -814,7 +823,6 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
                 NPGX_HIP(stream_wait(st));
             }
         }
-    }
     }
     NPGX_HIP(hipMemcpyAsync(hp, af->counters.p, 8, hipMemcpyDeviceToHost, st));
     NPGX_HIP(stream_wait(st));

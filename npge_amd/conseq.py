@@ -63,7 +63,10 @@ class DeConSeq(Processor):
         out = _engine(seqs, [])
         out.deconseq(cons, source=src)
         new = out.blocks()
-        names = [b.name for b in other.blocks] if len(new) == len(other.blocks) else [""] * len(new)
-        for blk, name in zip(new, names):
+        # one new block per consensus block, in order (empty ones included,
+        # DeConSeq.cpp:94-99): each keeps its consensus block's name
+        if len(new) != len(other.blocks):
+            raise _capi.NpgxError(-5, "DeConSeq: %d blocks for %d consensus blocks" % (len(new), len(other.blocks)))
+        for blk, name in zip(new, [b.name for b in other.blocks]):
             target.blocks.append(Block([Fragment(seqs[q], mn, mx, ori, row) for q, mn, mx, ori, row in blk],
                                        name=name))

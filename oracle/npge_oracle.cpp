@@ -2321,7 +2321,7 @@ int orc_bs_deconseq(orc_bs* target, const orc_bs* source, const orc_bs* cons) {
             if (cf.seq < 0 || (size_t)cf.seq >= source->bs.blocks.size()) return -1;
         try {
             orc::BBlock nb = orc::deconseq_block(source->seqs, source->bs.blocks, cb);
-            if (!nb.f.empty()) out.push_back(nb);
+            out.push_back(nb);  // empty ones too (DeConSeq.cpp:94-99 inserts every new block)
         } catch (const std::exception&) {
             return -2;
         }

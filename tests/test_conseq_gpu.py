@@ -65,6 +65,29 @@ def test_deconseq_kat_alignment():
     assert len(src.blocks()) == 3 and src.blocks()[2] == blk
 
 
+def test_deconseq_keeps_empty_blocks():
+    """DeConSeq inserts every new block, empty ones included
+    (DeConSeq.cpp:86-99): an empty consensus block maps to an empty block in
+    its place; engine and oracle agree."""
+    seqs, names = [S1, S2], ["a", "b"]
+    src_blocks = [[(0, 0, 7, 1, None), (1, 0, 6, 1, None)]]
+    src = _engine(seqs, names, src_blocks)
+    cs = src.conseq()
+    cons_blocks = [[(0, 0, 3, 1, None)], [], [(0, 2, 5, -1, None), (0, 0, 1, 1, None)]]
+    cons = _engine(cs, ["c"], cons_blocks)
+    tgt = _engine(seqs, names, [])
+    tgt.deconseq(cons, source=src)
+    got = tgt.blocks()
+    assert len(got) == 3 and got[1] == []
+    o_src = orc.BlockSetOracle(seqs, names)
+    o_src.set_blocks(src_blocks)
+    o_cons = orc.BlockSetOracle(cs, ["c"])
+    o_cons.set_blocks(cons_blocks)
+    o_tgt = orc.BlockSetOracle(seqs, names)
+    o_tgt.deconseq(o_cons, source=o_src)
+    assert got == o_tgt.blocks()
+
+
 def test_deconseq_mismatch_is_an_error():
     from npge_amd import _capi
     src = _engine([S1, S2], ["a", "b"], [[(0, 0, 7, 1, None), (1, 0, 6, 1, None)]])

@@ -2275,10 +2275,12 @@ struct npgx_aligner {
     // NPGX_ALIGN_DEFER=<columns>: alignments at least this long hand their bad
     // regions to k_align_sub (0: every bad region realigned inside its job)
     // deferred bad regions (sub-jobs of their own): alignments of at least
-    // this many columns and rows -- long many-row alignments gain (C3 17 rows:
-    // align 46.6 -> 45.0 ms at 8000 vs 1000 columns), 3-row ones only pay the
-    // extra launches (C2 align 11.1 -> 10.4 ms without)
-    int defer = 8000;
+    // this many columns and rows -- with long jobs split into segments the
+    // unsplit many-row jobs of a few hundred columns became a launch's tail
+    // (their bad regions re-aligned one after the other by one wave): C3
+    // align 19.3 -> 18.6 ms at 500 vs 8000 columns (tools/gpu_defer_sweep.sh);
+    // 3-row ones only pay the extra launches (defer_rows)
+    int defer = 500;
     int defer_rows = 4;
     DevBuf<int4> d_job_regions;
     DevBuf<int32_t> d_job_nreg, d_fin;
@@ -2893,6 +2895,35 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                             d[q].first / 100.0, r.y, r.x, splits[segs[(size_t)d[q].second].split].K,
                             jobs[splits[segs[(size_t)d[q].second].split].job].n);
                 }
+                // the launch's critical path: when the segments and the whole jobs end
+                std::vector<int64_t> js((size_t)n_jobs * NPGX_JOB_STATS);
+                NPGX_HIP(hipMemcpy(js.data(), al->d_job_stats.p, js.size() * 8, hipMemcpyDeviceToHost));
+                int64_t t0 = INT64_MAX, se = 0, je = 0, jd = 0;
+                int jslow = -1;
+                for (size_t q = 0; q < segs.size(); q++) {
+                    t0 = std::min(t0, sw[2 * q]);
+                    se = std::max(se, sw[2 * q + 1]);
+                }
+                std::vector<uint8_t> was_split(n_jobs, 0);
+                for (const SaSplit& sp2 : splits) was_split[sp2.job] = 1;
+                for (int32_t j : todo) {
+                    const int64_t* r = js.data() + (size_t)j * NPGX_JOB_STATS;
+                    if (was_split[j] || r[11] <= 0 || r[23] <= 0) continue;
+                    t0 = std::min(t0, r[11]);
+                    je = std::max(je, r[23]);
+                    if (r[23] - r[11] > jd) {
+                        jd = r[23] - r[11];
+                        jslow = j;
+                    }
+                }
+                if (t0 != INT64_MAX)
+                    fprintf(stderr, "launch: segments end at %.1f us, whole jobs at %.1f us; slowest whole job %d: "
+                            "%.1f us, %lld cols, %d rows (process_seqs %.1f us, regions+realign %.1f us)\n",
+                            (se - t0) / 100.0, (je - t0) / 100.0, jslow, jd / 100.0,
+                            jslow >= 0 ? (long long)js[(size_t)jslow * NPGX_JOB_STATS + 1] : 0ll,
+                            jslow >= 0 ? jobs[jslow].n : 0,
+                            jslow >= 0 ? js[(size_t)jslow * NPGX_JOB_STATS + 8] / 2400.0 : 0.0,
+                            jslow >= 0 ? js[(size_t)jslow * NPGX_JOB_STATS + 9] / 2400.0 : 0.0);
             }
             if (deferring) {  // sub-jobs: count and widths
                 unsigned long long al2[2];

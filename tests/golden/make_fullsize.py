@@ -3,7 +3,7 @@ af_digest / blocks_digest) of the CPU restatement's outputs on the C4 and C5
 synthetic sets (npge_amd/synth.py, seeded), which the oracle needs minutes for
 and which therefore cannot be recomputed inside a GPU test.
 
-    python tests/golden/make_fullsize.py [C4 C5 C5sub2 loop:C4 ...]
+    python tests/golden/make_fullsize.py [C4 C5 C5sub2 loop:C4 draft:C5 ...]
 
 Cases: <cfg> = the whole set; <cfg>subN = its first N sequences.  Each case
 records AnchorFinder (defaults, two runs on one instance so the persistent
@@ -62,6 +62,24 @@ def make(case):
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def add_draft(case):
+    """Only the DraftPangenome entry, into an existing fixture."""
+    names, seqs = case_input(case)
+    path = os.path.join(HERE, "fullsize", case + ".json")
+    with open(path) as f:
+        out = json.load(f)
+    t = time.time()
+    b = orc.BlockSetOracle(seqs, names)
+    b.set_workers(os.cpu_count() or 1)
+    b.apply("DraftPangenome")
+    st = b.stats()
+    out["draft"] = dict(blocks_digest(b.blocks()), hash=int(b.hash()),
+                        stats={k: int(v) for k, v in st.items()})
+    print(case, "DraftPangenome %.1f s" % (time.time() - t), flush=True)
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def add_loop(case):
     """Only the AnchorLoopFast entry, into an existing fixture."""
     names, seqs = case_input(case)
@@ -84,5 +102,7 @@ if __name__ == "__main__":
     for c in sys.argv[1:] or ["C4", "C5sub2", "C5"]:
         if c.startswith("loop:"):
             add_loop(c[5:])
+        elif c.startswith("draft:"):
+            add_draft(c[6:])
         else:
             make(c)

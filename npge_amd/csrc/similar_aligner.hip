@@ -130,6 +130,7 @@ struct SaArgs {
     int32_t* targets;          // sync states (k_split_find)
     int4* seg_res;             // per segment: next segment (K: ran to the end, -1: idle), columns, overflow
     int64_t* seg_wall;         // per segment: wall clock at start and end (job statistics)
+    int64_t* sub_wall;         // per whole sub-job: wall clock at start and end (job statistics)
     unsigned char* seg_pool;
     // sub-job splits (k_plan_subs): capacities of the arrays above and the
     // sub-job queue (segment tasks first, then whole sub-jobs)
@@ -925,6 +926,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             v.len = ((const int*)(a.pool + d.out_off))[lane] - start;
         }
         char* out = seg ? (char*)(a.seg_pool + sg.out) : (char*)(a.pool + d.out_off + 256);
+        const unsigned long long w_start = wall_clock64();
         Proc pr(w, a.P, e.S, out, seg ? sg.cap : d.out_cap, epoch, lepoch);
         int Lc = 0;
         bool ovf = false;
@@ -935,6 +937,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             ovf = any_lane(w, pr.ovf);
         }
         __syncthreads();
+        if (lane == 0 && a.job_stats) {  // (statistics wanted: the critical path of the launch)
+            int64_t* wl = seg ? a.seg_wall + 2 * (size_t)seg_t : (a.sub_wall ? a.sub_wall + 2 * (size_t)sn : nullptr);
+            if (wl) {
+                wl[0] = (int64_t)w_start;
+                wl[1] = (int64_t)wall_clock64();
+            }
+        }
         if (seg) {
             if (lane == 0)
                 a.seg_res[seg_t] = idle ? make_int4(-1, 0, 0, 0)
@@ -2313,6 +2322,7 @@ struct npgx_aligner {
     DevBuf<int32_t> d_targets;
     DevBuf<int4> d_seg_res;
     DevBuf<int64_t> d_seg_wall;
+    DevBuf<int64_t> d_sub_wall;
     DevBuf<int32_t> d_qseg, d_qsub;
     DevBuf<unsigned int> d_sctr;
     DevBuf<unsigned char> d_seg_pool;
@@ -2706,6 +2716,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.targets = nullptr;
         A.seg_res = nullptr;
         A.seg_wall = nullptr;
+        A.sub_wall = nullptr;
         A.seg_pool = nullptr;
         A.sctr = nullptr;
         A.qseg = nullptr;
@@ -2771,6 +2782,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A.targets = al->d_targets.p;
             A.seg_res = al->d_seg_res.p;
             A.seg_wall = al->d_seg_wall.p;
+            if (al->want_stats && deferring) {
+                al->d_sub_wall.grow(2 * (size_t)std::max<int64_t>(1, n_sub_max));
+                NPGX_HIP(hipMemsetAsync(al->d_sub_wall.p, 0, 2 * (size_t)std::max<int64_t>(1, n_sub_max) * 8, st));
+                A.sub_wall = al->d_sub_wall.p;
+            }
             A.seg_pool = al->d_seg_pool.p;
             A.sctr = al->d_sctr.p;
             A.qseg = al->d_qseg.p;
@@ -2933,6 +2949,35 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 if (!sb.empty()) {
                     NPGX_HIP(hipMemcpy(sb.data(), al->d_subs.p, sb.size() * sizeof(SaSub), hipMemcpyDeviceToHost));
                     NPGX_HIP(hipMemcpy(rs.data(), al->d_sub_res.p, rs.size() * 8, hipMemcpyDeviceToHost));
+                }
+                if (al->want_stats && A.sub_wall && !sb.empty()) {  // the sub-job launch's critical path
+                    std::vector<int64_t> sw2(2 * sb.size());
+                    NPGX_HIP(hipMemcpy(sw2.data(), al->d_sub_wall.p, sw2.size() * 8, hipMemcpyDeviceToHost));
+                    unsigned int sc2[SC_N];
+                    NPGX_HIP(hipMemcpy(sc2, al->d_sctr.p, sizeof(sc2), hipMemcpyDeviceToHost));
+                    std::vector<int64_t> segw(2 * (size_t)std::max(1, A.cap_segs));
+                    NPGX_HIP(hipMemcpy(segw.data(), al->d_seg_wall.p, segw.size() * 8, hipMemcpyDeviceToHost));
+                    int64_t t0 = INT64_MAX, wend = 0, send = 0, wmax = 0;
+                    int wslow = -1;
+                    for (size_t q = 0; q < sb.size(); q++)
+                        if (sw2[2 * q] > 0) {
+                            t0 = std::min(t0, sw2[2 * q]);
+                            wend = std::max(wend, sw2[2 * q + 1]);
+                            if (sw2[2 * q + 1] - sw2[2 * q] > wmax) {
+                                wmax = sw2[2 * q + 1] - sw2[2 * q];
+                                wslow = (int)q;
+                            }
+                        }
+                    for (unsigned int q = (unsigned int)segs.size(); q < std::min(sc2[SC_SEGS], (unsigned)A.cap_segs); q++)
+                        if (segw[2 * q] > 0) {
+                            t0 = std::min(t0, segw[2 * q]);
+                            send = std::max(send, segw[2 * q + 1]);
+                        }
+                    if (t0 != INT64_MAX)
+                        fprintf(stderr, "sub launch: %u sub segments end at %.1f us, whole subs at %.1f us; slowest whole "
+                                "sub %d: %.1f us, %d cols, %d rows\n", sc2[SC_SEGS] - (unsigned)segs.size(),
+                                send ? (send - t0) / 100.0 : 0.0, (wend - t0) / 100.0, wslow, wmax / 100.0,
+                                wslow >= 0 ? rs[(size_t)wslow].x : 0, wslow >= 0 ? jobs[sb[(size_t)wslow].job].n : 0);
                 }
                 std::vector<int> wd;
                 for (const int2& r : rs) wd.push_back(r.x);

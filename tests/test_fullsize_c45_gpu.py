@@ -77,7 +77,7 @@ def test_anchor_finder_c45(case):
             _check_properties(r, seqs)
 
 
-@pytest.mark.parametrize("case", ["C4", "C5sub2"])
+@pytest.mark.parametrize("case", ["C4", "C5sub2", "C5"])
 def test_draft_pangenome_c45(case):
     from npge_amd import _capi
     from npge_amd.anchor_finder import AnchorFinder

@@ -169,15 +169,19 @@ class Write(RawWrite):
     name = "Write"
 
 
+_COMP = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N"}
+
+
 def _complete_sequences(bs):
     """Fragment-only inputs (the expected-output style fixtures) name their
     sequences without text: give each one text long enough for its fragments,
     the rows' letters where rows cover it and 'A' elsewhere."""
-    need = {}
+    need = {}  # id(sequence) -> [sequence, length needed]
     for b in bs.blocks:
         for f in b.fragments:
             if not f.seq.data:
-                need.setdefault(id(f.seq), [f.seq, 0])[1] = max(need.get(id(f.seq), [f.seq, 0])[1], f.max_pos + 1)
+                entry = need.setdefault(id(f.seq), [f.seq, 0])
+                entry[1] = max(entry[1], f.max_pos + 1)
     for seq, n in need.values():
         text = ["A"] * n
         for b in bs.blocks:
@@ -186,8 +190,7 @@ def _complete_sequences(bs):
                     continue
                 letters = [c for c in f.row if c != "-"]
                 if f.ori == -1:
-                    comp = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N"}
-                    letters = [comp.get(c, "N") for c in reversed(letters)]
+                    letters = [_COMP.get(c, "N") for c in reversed(letters)]
                 for i, c in enumerate(letters[:f.max_pos - f.min_pos + 1]):
                     text[f.min_pos + i] = c
         seq.data = "".join(text)

@@ -94,7 +94,7 @@ def test_sharded_equals_single(world, config, maxf, similar, staging):
             np.testing.assert_array_equal(a["used"], b["used"])
 
 
-def _bb_worker(rank, world, port, config, out):
+def _bb_worker(rank, world, port, config, out, loop=False):
     import torch.distributed as dist
     from npge_amd import _capi, synth
     from npge_amd.comm import TorchComm
@@ -106,13 +106,13 @@ def _bb_worker(rank, world, port, config, out):
     names, seqs = synth.genome_set(config)
     ss = _capi.SeqSet(seqs, names)
     comm = TorchComm(dist, staging="cpu")
-    job = BlockBuild(ss, names, seqs, comm=comm)
+    job = BlockBuild(ss, names, seqs, comm=comm, anchor_loop=loop)
     info = job.run()
     st = job.eng.stats()
     got = (job.eng.hash(), job.eng.blocks(), info["align_jobs"], st["anchor_blocks"])
     ref = None
     if rank == 0:
-        one = BlockBuild(ss, names, seqs)
+        one = BlockBuild(ss, names, seqs, anchor_loop=loop)
         one.run()
         ref = (one.eng.hash(), one.eng.blocks(), one.eng.stats()["anchor_blocks"])
     out[rank] = (got, ref)
@@ -137,5 +137,21 @@ def test_sharded_draft_pangenome_equals_single(world, config):
         (h, blocks, n_jobs, anchors) = out[r][0]
         assert n_jobs > 0 or config == "C4"
         assert anchors == ref_anchors, "rank %d" % r
+        assert h == ref_hash, "rank %d" % r
+        assert blocks == ref_blocks, "rank %d" % r
+
+
+@pytest.mark.parametrize("world,config", [(2, "small"), (3, "tiny"), (2, "C4")])
+def test_sharded_anchor_loop_equals_single(world, config):
+    """DraftPangenome then AnchorLoopFast with a comm set: the consensus pipe's
+    AnchorFinder runs sharded and its FragmentsExtender batches are split over
+    the ranks (C4: whole-genome jobs); every rank ends with one GPU's blocks."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bb_worker, args=(world, _free_port(), config, out, True), nprocs=world, join=True)
+    ref_hash, ref_blocks, _ = out[0][1]
+    assert len(ref_blocks) > 0
+    for r in range(world):
+        (h, blocks, _, _) = out[r][0]
         assert h == ref_hash, "rank %d" % r
         assert blocks == ref_blocks, "rank %d" % r

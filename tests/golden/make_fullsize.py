@@ -22,8 +22,8 @@ from oracle import oracle as orc  # noqa: E402
 from npge_amd import synth  # noqa: E402
 from helpers import af_digest, blocks_digest, oracle_anchor_loop  # noqa: E402
 
-DP_CASES = {"C4", "C5sub2"}
-LOOP_CASES = {"C4"}  # DraftPangenome -> AnchorLoopFast
+DP_CASES = {"C3", "C4", "C5sub2"}
+LOOP_CASES = {"C3", "C4"}  # DraftPangenome -> AnchorLoopFast
 
 
 def case_input(case):

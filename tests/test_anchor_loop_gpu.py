@@ -95,3 +95,49 @@ def test_fragments_extender_portion_option():
         ref.set_blocks(start)
         ref.apply("FragmentsExtender")
         assert canon(eng.blocks()) == canon(ref.blocks())
+
+
+def _repeat_genomes(copies, genomes=2, unit=300, seed=5):
+    """Genomes of random sequence with `copies` slightly mutated copies of one
+    repeat unit each (an IS-element-like family)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    rep = rng.integers(0, 4, unit)
+    names, seqs = [], []
+    for g in range(genomes):
+        parts = []
+        for _ in range(copies):
+            parts.append(rng.integers(0, 4, int(rng.integers(200, 400))))
+            r = rep.copy()
+            m = rng.random(unit) < 0.01
+            r[m] = (r[m] + rng.integers(1, 4, int(m.sum()))) % 4
+            parts.append(r)
+        s = np.concatenate(parts)
+        names.append("G%02d&chr1&c" % (g + 1))
+        seqs.append("".join("ATGC"[x] for x in s))
+    return names, seqs
+
+
+def test_more_than_64_rows_fail_loudly():
+    """The aligner's lanes are rows: a block of more than 64 fragments (a
+    repeat family across genomes) is refused with NPGX_ERR_RANGE instead of
+    being cut -- MetaAligner on such a block and AnchorLoopFast on genomes
+    carrying 40 copies each (80-fragment anchors).  With 30 copies per genome
+    (60 fragments) the same pipe runs and matches the oracle."""
+    from npge_amd import _capi
+    from npge_amd.anchor_finder import AnchorFinder
+    from npge_amd.anchor_loop import anchor_loop_fast
+    names, seqs = _repeat_genomes(40)
+    eng = _engine(seqs, names, [])
+    with pytest.raises(_capi.NpgxError) as e:
+        anchor_loop_fast(eng, AnchorFinder())
+    assert e.value.code == -4 and "64" in str(e.value)
+    names, seqs = _repeat_genomes(30)
+    eng = _engine(seqs, names, [])
+    st = anchor_loop_fast(eng, AnchorFinder())
+    o = orc.BlockSetOracle(seqs, names)
+    o.set_blocks([])
+    ost = _oracle_loop(o)
+    assert st["anchors"] > 0
+    assert st["loop_iterations"] == ost["iterations"]
+    assert canon(eng.blocks()) == canon(o.blocks())

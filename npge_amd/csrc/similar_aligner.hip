@@ -2412,6 +2412,15 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         max_len = std::max(max_len, mx);
         max_cap = std::max<int>(max_cap, J.cap);
     }
+    static const bool pdbg = getenv("NPGX_PREP_DEBUG") != nullptr;  // host phase times to stderr
+    double pt[12] = {0};
+    auto pt0 = std::chrono::steady_clock::now();
+    auto pmark = [&](int i) {
+        if (!pdbg) return;
+        pt[i] += ms(pt0);
+        pt0 = std::chrono::steady_clock::now();
+    };
+    pmark(0);
     // heaviest first (rows x residues), by power-of-two cost classes: the order
     // only balances the load, results do not depend on it
     std::vector<int32_t>& order = al->h_order;
@@ -2434,6 +2443,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         for (int32_t j = 0; j < n_jobs; j++) order[at[cls[j]]++] = j;
     }
 
+    pmark(1);
     al->d_row_off.ensure(ne_off.size());
     al->d_row_len.ensure(ne_len.size());
     al->d_jobs.ensure(jobs.size());
@@ -2483,6 +2493,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 max_cap = std::max<int>(max_cap, J.cap);
             }
         }
+        pmark(2);
         // the work queue: the segments of the split jobs (heaviest first), then
         // the other jobs
         std::vector<SaSplit>& splits = al->h_splits;
@@ -2553,6 +2564,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->d_order.grow(queue.size());
         put(al->d_order.p, queue.data(), queue.size() * 4);
         NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
+        pmark(3);
         // per-slot scratch: the word table (20 B an entry), the append_aligned
         // stack (1028 B a level) and the regions of unsplit jobs (17 B a
         // column), for SA_WAVES_PER_EU waves on each of the 4 SIMDs of the 256
@@ -2603,6 +2615,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->regions.ensure(slots * (size_t)slot_cols);
         al->good_col.ensure(slots * (size_t)slot_cols);
 
+        pmark(4);
         SaArgs A;
         A.rows = d_rows;
         A.row_off = al->d_row_off.p;
@@ -2675,6 +2688,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A.max_sub = 0;
             A.fin = nullptr;
         }
+        pmark(5);
         // LDS: word table (20 B/entry) + the largest job's rows.  A workgroup may
         // take all 160 KiB of a CU's LDS; when the batch has more jobs than
         // workgroups can be resident at that size the stage shrinks, and the
@@ -2800,6 +2814,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 al->timer.end(tf, st);
             }
         }
+        pmark(6);
         int64_t residues = 0;
         for (int32_t j : todo) residues += jsum[j];
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
@@ -2807,6 +2822,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
+        pmark(7);
         if (!splits.empty()) {  // the split jobs: chain, regions, deferred bad regions
             ti = al->timer.begin("align_split_chain", st, 0.0, (int64_t)splits.size());
             hipLaunchKernelGGL(k_split_chain, dim3((unsigned)splits.size()), dim3(POST_THREADS), 0, st, A);
@@ -2989,6 +3005,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                         wd.empty() ? 0 : wd[wd.size() * 99 / 100], wd.empty() ? 0 : wd.back());
             }
         }
+        pmark(8);
         int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);
         NPGX_HIP(hipMemcpyAsync(pl, al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
         NPGX_HIP(hipMemcpyAsync(pl + n_jobs, al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
@@ -3004,6 +3021,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         memcpy(jstat.data(), pl + n_jobs, n_jobs * 4);
         al->epoch_base = std::max(al->epoch_base, (uint32_t)pl[2 * n_jobs] + 1);
         al->pinned.reset();
+        pmark(9);
         std::vector<int32_t> again;
         for (int32_t j : todo) {
             NPGX_REQUIRE(jstat[j] >= 0 && jstat[j] <= 2, NPGX_ERR_STATE, "alignment job left unfinished");
@@ -3024,6 +3042,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         todo.swap(again);
     }
     al->host_ms[0] += ms(tp);
+    pmark(10);
+    if (pdbg)
+        fprintf(stderr, "align_device %d jobs: prep %.3f order %.3f puts %.3f split_plan %.3f slots %.3f args %.3f "
+                "lds+split %.3f launch %.3f post %.3f wait %.3f results %.3f ms\n", n_jobs, pt[0], pt[1], pt[2],
+                pt[3], pt[4], pt[5], pt[6], pt[7], pt[8], pt[9], pt[10]);
 }
 
 void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,

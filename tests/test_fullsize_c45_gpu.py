@@ -1,5 +1,5 @@
 """Parity at BASELINE.json's C4 (32 x 5 Mbp, 2 % divergence) and C5
-(8 x 50 Mbp, 1 %) sizes.  The CPU restatement needs minutes there, so its
+(8 x 50 Mbp, 1 %) sizes, and AnchorLoopFast at C3 and C4.  The CPU restatement needs minutes there, so its
 outputs are committed as fingerprints (tests/golden/fullsize/*.json, made by
 tests/golden/make_fullsize.py; tests/helpers.py af_digest / blocks_digest):
 the GPU run's SoA anchor set, Bloom parameters, counts and persistent used-hash
@@ -94,16 +94,18 @@ def test_draft_pangenome_c45(case):
     assert got == want, _diff(got, want)
 
 
-def test_anchor_loop_c4():
-    """DraftPangenome -> AnchorLoopFast at C4 (the bench's --anchor-loop
-    workload): on the 32 genome-long consensus sequences the pipe's
-    ExtendLoopFast grows whole-genome blocks (alignments of millions of
-    columns, split into segments), 18 iterations; blocks, rows and
-    blockset_hash equal the oracle pipe's (fixture: 250 s on the CPU)."""
+@pytest.mark.parametrize("case", ["C3", "C4"])
+def test_anchor_loop_fullsize(case):
+    """DraftPangenome -> AnchorLoopFast (the bench's --anchor-loop workload).
+    C4: on the 32 genome-long consensus sequences the pipe's ExtendLoopFast
+    grows whole-genome blocks (alignments of millions of columns, split into
+    segments), 18 iterations (fixture: 250 s on the CPU); C3: the 17-genome
+    draft's consensus blocks.  Blocks, rows and blockset_hash equal the oracle
+    pipe's."""
     from npge_amd import _capi
     from npge_amd.anchor_finder import AnchorFinder
     from npge_amd.blockset import BlockSetEngine
-    names, seqs, gold = _case("C4")
+    names, seqs, gold = _case(case)
     eng = BlockSetEngine(_capi.SeqSet(seqs, names))
     eng.apply("DraftPangenome", af=AnchorFinder())
     eng.apply("AnchorLoopFast", af=AnchorFinder())

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <memory>
 #include <numeric>
 
 #include "common.hpp"
@@ -249,10 +250,19 @@ int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char*
                 d_ao.ensure(n);
                 d_no.ensure(n);
                 d_sz.ensure(n);
-                for (int32_t r = 0; r < n; r++) {  // every sequence straight to its place
-                    const std::string& d = s->data[s->by_rank[r]];
-                    if (!d.empty())
-                        NPGX_HIP(hipMemcpy(d_ascii.p + ascii_off[r], d.data(), d.size(), hipMemcpyHostToDevice));
+                if (n <= 256) {  // few (long) sequences: each straight to its place
+                    for (int32_t r = 0; r < n; r++) {
+                        const std::string& d = s->data[s->by_rank[r]];
+                        if (!d.empty())
+                            NPGX_HIP(hipMemcpy(d_ascii.p + ascii_off[r], d.data(), d.size(), hipMemcpyHostToDevice));
+                    }
+                } else {  // many: gathered on host threads, one copy
+                    std::unique_ptr<char[]> cat(new char[(size_t)ao]);
+                    heavy_for((size_t)n, ao, [&](size_t r) {
+                        const std::string& d = s->data[s->by_rank[r]];
+                        memcpy(cat.get() + ascii_off[r], d.data(), d.size());
+                    });
+                    NPGX_HIP(hipMemcpy(d_ascii.p, cat.get(), (size_t)ao, hipMemcpyHostToDevice));
                 }
                 NPGX_HIP(hipMemcpy(d_wo.p, s->word_off.data(), n * 8, hipMemcpyHostToDevice));
                 NPGX_HIP(hipMemcpy(d_ao.p, ascii_off.data(), n * 8, hipMemcpyHostToDevice));

@@ -1860,6 +1860,24 @@ struct PipelineStats {
 };
 
 // ExtendLoopFast (lua_lib.lua:697-709) under Pipe::run_impl (Pipe.cpp:60-78)
+// OverlaplessUnion --ou-move into an empty target (OverlaplessUnion.cpp:55-77):
+// blocks in ou_before order (ties: input order), admitted greedily if no
+// fragment overlaps an admitted one
+static void overlapless_union(std::vector<BBlock>& blocks) {
+    std::vector<size_t> order(blocks.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return ou_before(blocks[a], blocks[b]); });
+    OverlapIndex idx;
+    std::vector<BBlock> ol;
+    for (size_t i : order) {
+        if (!idx.block_has_overlap(blocks[i])) {
+            idx.add(blocks[i]);
+            ol.push_back(std::move(blocks[i]));
+        }
+    }
+    blocks.swap(ol);
+}
+
 static void extend_loop_fast(BlockSetO& bs, const PipelineOpts& o, PipelineStats& st) {
     const std::vector<BSeq>& seqs = *bs.seqs;
     std::set<uint64_t> seen_states;
@@ -1902,20 +1920,9 @@ static void extend_loop_fast(BlockSetO& bs, const PipelineOpts& o, PipelineStats
         // Move target=target other=unchanged
         for (BBlock& b : unchanged) fixed.push_back(std::move(b));
         // OverlaplessUnion target=ol other=target --ou-move:=1
-        std::vector<size_t> order(fixed.size());
-        for (size_t i = 0; i < order.size(); i++) order[i] = i;
-        std::stable_sort(order.begin(), order.end(),
-                         [&](size_t a, size_t b) { return ou_before(fixed[a], fixed[b]); });
-        OverlapIndex idx;
-        std::vector<BBlock> ol;
-        for (size_t i : order) {
-            if (!idx.block_has_overlap(fixed[i])) {
-                idx.add(fixed[i]);
-                ol.push_back(std::move(fixed[i]));
-            }
-        }
+        overlapless_union(fixed);
         // Clear target; Move target=target other=ol; Clear ol
-        bs.blocks.swap(ol);
+        bs.blocks.swap(fixed);
         uint64_t h = blockset_hash(bs);
         if (seen_states.count(h)) break;
         seen_states.insert(h);
@@ -2192,7 +2199,8 @@ void orc_bs_set_workers(orc_bs* h, int workers) { h->af.workers = h->po.workers 
 
 // op: 0 FragmentsExtender, 1 FixEnds, 2 Filter, 3 ExtendLoopFast, 4 DummyAligner,
 // 5 RemoveNonStem --exact, 6 DraftPangenome (AnchorFinder on all sequences first),
-// 7 MetaAligner(similar) align_block, 8 Filter::find_good_subblocks, 9 Rest
+// 7 MetaAligner(similar) align_block, 8 Filter::find_good_subblocks, 9 Rest,
+// 10 OverlaplessUnion --ou-move
 int orc_bs_apply(orc_bs* h, int op) {
     const std::vector<orc::BSeq>& seqs = h->seqs;
     orc::PipelineOpts& o = h->po;
@@ -2239,6 +2247,9 @@ int orc_bs_apply(orc_bs* h, int op) {
             return 0;
         case 9:
             orc::rest(seqs, h->bs.blocks);
+            return 0;
+        case 10:
+            orc::overlapless_union(h->bs.blocks);
             return 0;
         case 8:  // Filter::find_good_subblocks only
             for (auto& b : h->bs.blocks) orc::filter_subblocks(seqs, b, o.filter, out);

@@ -286,7 +286,7 @@ _PKEYS = list(PIPELINE_DEFAULTS)
 
 OPS = {"FragmentsExtender": 0, "FixEnds": 1, "Filter": 2, "ExtendLoopFast": 3, "DummyAligner": 4,
        "RemoveNonStem": 5, "DraftPangenome": 6, "MetaAligner": 7, "FindGoodSubblocks": 8,
-       "Rest": 9}
+       "Rest": 9, "OverlaplessUnion": 10}
 
 
 def _bs_lib():

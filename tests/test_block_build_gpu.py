@@ -167,3 +167,42 @@ def test_meta_aligner(cfg):
     got = eng.blocks()
     assert got == o.blocks()
     assert any("-" in (f[4] or "") for b in got for f in b)
+
+
+def _ou_blocks(rng, n_seqs, seq_len, n_blocks, max_len, self_overlap=False):
+    blocks = []
+    for _ in range(n_blocks):
+        k = int(rng.integers(1, min(n_seqs, 6) + 1))
+        frs = []
+        for s in rng.choice(n_seqs, size=k, replace=False):
+            mn = int(rng.integers(0, seq_len - max_len))
+            frs.append((int(s), mn, mn + int(rng.integers(0, max_len)), int(rng.choice([-1, 1])), None))
+        blocks.append(frs)
+    if self_overlap:  # a block overlapping itself: the ordered multiset mode
+        s, mn, mx, ori, _ = blocks[7][0]
+        blocks[7].append((s, mn, mx + 5, -ori, None))
+    return blocks
+
+
+@pytest.mark.parametrize("max_len,self_overlap", [(40, False), (400, False), (3000, False), (40, True)])
+def test_overlapless_union_many_blocks(max_len, self_overlap):
+    """OverlaplessUnion --ou-move over 1500 blocks: sparse (the threaded
+    conflict pre-pass admits most blocks directly), dense (most rejected),
+    long fragments past the interval-map threshold, and a self-overlapping
+    block (pre-pass declines); then a second call on the same engine, which
+    after a high rejection rate takes the ordered test for every block."""
+    import numpy as np
+    rng = np.random.default_rng(max_len + self_overlap)
+    n_seqs, seq_len = 8, 400000
+    seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
+    names = ["g%d&c&c" % i for i in range(n_seqs)]
+    blocks = _ou_blocks(rng, n_seqs, seq_len, 1500, max_len, self_overlap)
+    ss, eng = _engine(seqs, names)
+    o = orc.BlockSetOracle(seqs, names)
+    for rnd in range(2):
+        eng.set_blocks(blocks).apply("OverlaplessUnion")
+        o.set_blocks(blocks)
+        o.apply("OverlaplessUnion")
+        want = o.blocks()
+        assert eng.blocks() == want, rnd
+        assert 0 < len(want) <= len(blocks)

@@ -12,6 +12,7 @@
 // Sequences are stored in processing (rank) order: size desc, name asc, input
 // index asc (the pinned form of SeqI.hpp:54).
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <memory>
@@ -115,6 +116,71 @@ hipError_t stream_wait(hipStream_t s) {
     return e;
 }
 
+// Rank (size desc, name asc, input index asc), layout and the packed words /
+// N bitmap of s, whose sequence i (s->data[i], ATGCN only) also sits on the
+// device at d_ascii + ascii[i].
+void pack_device(npgx_seqset* s, const unsigned char* d_ascii, const std::vector<int64_t>& ascii) {
+    const int32_t n = s->n;
+    s->by_rank.resize(n);
+    std::iota(s->by_rank.begin(), s->by_rank.end(), 0);
+    std::sort(s->by_rank.begin(), s->by_rank.end(), [&](int32_t a, int32_t b) {
+        if (s->data[a].size() != s->data[b].size()) return s->data[a].size() > s->data[b].size();
+        if (s->names[a] != s->names[b]) return s->names[a] < s->names[b];
+        return a < b;
+    });
+    s->rank_of.assign(n, 0);
+    for (int32_t r = 0; r < n; r++) s->rank_of[s->by_rank[r]] = r;
+    s->word_off.resize(n);
+    s->n_off.resize(n);
+    std::vector<int64_t> ascii_off(n), size_r(n);
+    int64_t wo = 0, no = 0;
+    for (int32_t r = 0; r < n; r++) {
+        const int32_t i = s->by_rank[r];
+        const int64_t sz = (int64_t)s->data[i].size();
+        int64_t nw = (sz + 31) / 32 + 1;  // + zero pad word
+        if (nw % 2) nw += 1;              // keep N-word pairing aligned
+        s->word_off[r] = wo;
+        s->n_off[r] = no;
+        ascii_off[r] = ascii[i];
+        size_r[r] = sz;
+        wo += nw;
+        no += nw / 2;
+    }
+    s->total_words = wo;
+    s->total_nwords = no;
+    s->words.ensure((size_t)wo);
+    s->nmask.ensure((size_t)no);
+    if (wo == 0) return;
+    // the four per-rank tables in one upload
+    std::vector<int64_t> tab(4 * (size_t)n);
+    std::copy(s->word_off.begin(), s->word_off.end(), tab.begin());
+    std::copy(ascii_off.begin(), ascii_off.end(), tab.begin() + n);
+    std::copy(s->n_off.begin(), s->n_off.end(), tab.begin() + 2 * (size_t)n);
+    std::copy(size_r.begin(), size_r.end(), tab.begin() + 3 * (size_t)n);
+    DevBuf<int64_t> d_tab;
+    d_tab.ensure(tab.size());
+    NPGX_HIP(hipMemcpy(d_tab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
+    NPGX_HIP(hipMemset(s->nmask.p, 0, (size_t)no * 8));
+    const int threads = 256;
+    const int64_t blocks = (wo + threads - 1) / threads;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(threads), 0, 0, d_ascii, d_tab.p, d_tab.p + n,
+                       d_tab.p + 2 * n, d_tab.p + 3 * n, n, wo, s->words.p, s->nmask.p);
+    NPGX_HIP(hipGetLastError());
+    NPGX_HIP(hipDeviceSynchronize());
+}
+
+npgx_seqset* seqset_from_device(const char* host_text, const char* d_text, const std::vector<int64_t>& off) {
+    const int32_t n = (int32_t)off.size() - 1;
+    std::unique_ptr<npgx_seqset> s(new npgx_seqset);
+    s->device = current_device_checked();
+    s->n = n;
+    s->names.resize(n);
+    s->data.resize(n);
+    heavy_for((size_t)n, off[n], [&](size_t i) { s->data[i].assign(host_text + off[i], (size_t)(off[i + 1] - off[i])); });
+    pack_device(s.get(), (const unsigned char*)d_text, off);
+    return s.release();
+}
+
 HostPool::HostPool(int threads) {
     for (int i = 1; i < threads; i++) workers_.emplace_back([this] { loop(); });
 }
@@ -197,91 +263,37 @@ int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char*
         NPGX_REQUIRE(out && n >= 0 && (n == 0 || (seqs && lens)), NPGX_ERR_ARG,
                      "npgx_seqset_create: bad arguments");
         int dev = current_device_checked();
-        auto* s = new npgx_seqset;
-        try {
-            s->device = dev;
-            s->n = n;
-            s->names.resize(n);
-            s->data.resize(n);
-            int64_t total = 0;
-            for (int32_t i = 0; i < n; i++) {
-                NPGX_REQUIRE(lens[i] >= 0, NPGX_ERR_ARG, "negative sequence length");
-                s->names[i] = names && names[i] ? names[i] : "";
-                total += lens[i];
-            }
-            heavy_for((size_t)n, total, [&](size_t i) { s->data[i] = to_atgcn(seqs[i], lens[i]); });
-            // rank: size desc, name asc, input index asc
-            s->by_rank.resize(n);
-            std::iota(s->by_rank.begin(), s->by_rank.end(), 0);
-            std::sort(s->by_rank.begin(), s->by_rank.end(), [&](int32_t a, int32_t b) {
-                if (s->data[a].size() != s->data[b].size())
-                    return s->data[a].size() > s->data[b].size();
-                if (s->names[a] != s->names[b]) return s->names[a] < s->names[b];
-                return a < b;
-            });
-            s->rank_of.assign(n, 0);
-            for (int32_t r = 0; r < n; r++) s->rank_of[s->by_rank[r]] = r;
-            // layout
-            s->word_off.resize(n);
-            s->n_off.resize(n);
-            std::vector<int64_t> ascii_off(n), size_r(n);
-            int64_t wo = 0, no = 0, ao = 0;
-            for (int32_t r = 0; r < n; r++) {
-                int64_t sz = (int64_t)s->data[s->by_rank[r]].size();
-                int64_t nw = (sz + 31) / 32 + 1;           // + zero pad word
-                if (nw % 2) nw += 1;                       // keep N-word pairing aligned
-                s->word_off[r] = wo;
-                s->n_off[r] = no;
-                ascii_off[r] = ao;
-                size_r[r] = sz;
-                wo += nw;
-                no += nw / 2;
-                ao += sz;
-            }
-            s->total_words = wo;
-            s->total_nwords = no;
-            s->words.ensure((size_t)wo);
-            s->nmask.ensure((size_t)no);
-            if (wo > 0) {
-                DevBuf<unsigned char> d_ascii;
-                DevBuf<int64_t> d_wo, d_ao, d_no, d_sz;
-                d_ascii.ensure((size_t)std::max<int64_t>(ao, 1));
-                d_wo.ensure(n);
-                d_ao.ensure(n);
-                d_no.ensure(n);
-                d_sz.ensure(n);
-                if (n <= 256) {  // few (long) sequences: each straight to its place
-                    for (int32_t r = 0; r < n; r++) {
-                        const std::string& d = s->data[s->by_rank[r]];
-                        if (!d.empty())
-                            NPGX_HIP(hipMemcpy(d_ascii.p + ascii_off[r], d.data(), d.size(), hipMemcpyHostToDevice));
-                    }
-                } else {  // many: gathered on host threads, one copy
-                    std::unique_ptr<char[]> cat(new char[(size_t)ao]);
-                    heavy_for((size_t)n, ao, [&](size_t r) {
-                        const std::string& d = s->data[s->by_rank[r]];
-                        memcpy(cat.get() + ascii_off[r], d.data(), d.size());
-                    });
-                    NPGX_HIP(hipMemcpy(d_ascii.p, cat.get(), (size_t)ao, hipMemcpyHostToDevice));
-                }
-                NPGX_HIP(hipMemcpy(d_wo.p, s->word_off.data(), n * 8, hipMemcpyHostToDevice));
-                NPGX_HIP(hipMemcpy(d_ao.p, ascii_off.data(), n * 8, hipMemcpyHostToDevice));
-                NPGX_HIP(hipMemcpy(d_no.p, s->n_off.data(), n * 8, hipMemcpyHostToDevice));
-                NPGX_HIP(hipMemcpy(d_sz.p, size_r.data(), n * 8, hipMemcpyHostToDevice));
-                NPGX_HIP(hipMemset(s->nmask.p, 0, (size_t)no * 8));
-                int threads = 256;
-                int64_t blocks = (wo + threads - 1) / threads;
-                hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(threads), 0, 0, d_ascii.p,
-                                   d_wo.p, d_ao.p, d_no.p, d_sz.p, n, wo, s->words.p,
-                                   s->nmask.p);
-                NPGX_HIP(hipGetLastError());
-                NPGX_HIP(hipDeviceSynchronize());
-            }
-            *out = s;
-        } catch (...) {
-            delete s;
-            throw;
+        std::unique_ptr<npgx_seqset> s(new npgx_seqset);
+        s->device = dev;
+        s->n = n;
+        s->names.resize(n);
+        s->data.resize(n);
+        int64_t total = 0;
+        for (int32_t i = 0; i < n; i++) {
+            NPGX_REQUIRE(lens[i] >= 0, NPGX_ERR_ARG, "negative sequence length");
+            s->names[i] = names && names[i] ? names[i] : "";
+            total += lens[i];
         }
+        heavy_for((size_t)n, total, [&](size_t i) { s->data[i] = to_atgcn(seqs[i], lens[i]); });
+        // the ASCII text on the device in input order, then packed
+        std::vector<int64_t> ascii(n + 1, 0);
+        for (int32_t i = 0; i < n; i++) ascii[i + 1] = ascii[i] + (int64_t)s->data[i].size();
+        DevBuf<unsigned char> d_ascii;
+        d_ascii.ensure((size_t)std::max<int64_t>(ascii[n], 1));
+        if (n <= 256) {  // few (long) sequences: each straight to its place
+            for (int32_t i = 0; i < n; i++)
+                if (!s->data[i].empty())
+                    NPGX_HIP(hipMemcpy(d_ascii.p + ascii[i], s->data[i].data(), s->data[i].size(),
+                                       hipMemcpyHostToDevice));
+        } else if (ascii[n] > 0) {  // many: gathered on host threads, one copy
+            std::unique_ptr<char[]> cat(new char[(size_t)ascii[n]]);
+            heavy_for((size_t)n, ascii[n], [&](size_t i) {
+                memcpy(cat.get() + ascii[i], s->data[i].data(), s->data[i].size());
+            });
+            NPGX_HIP(hipMemcpy(d_ascii.p, cat.get(), (size_t)ascii[n], hipMemcpyHostToDevice));
+        }
+        pack_device(s.get(), d_ascii.p, ascii);
+        *out = s.release();
     });
 }
 

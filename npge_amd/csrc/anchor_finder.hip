@@ -323,11 +323,13 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
                         pw[i] = (pw[i] >> (idx[i] & 31)) & 1u;  // set by an earlier epoch
                         fv[i] = pw[i] ? 0u : first[idx[i]];
                     }
+                // a bit new in this epoch goes into Pn once, by its first
+                // setter (first[] holds that window's order)
 #pragma unroll
                 for (int i = 0; i < FKB; i++)
                     if (i < a.kb && !pw[i]) {
                         f &= fv[i] < ord;
-                        if (Pn) atomicOr(&Pn[idx[i] >> 5], 1u << (idx[i] & 31));
+                        if (Pn && fv[i] == ord) atomicOr(&Pn[idx[i] >> 5], 1u << (idx[i] & 31));
                     }
             } else {
                 for (int i = 0; i < a.kb; i++) {

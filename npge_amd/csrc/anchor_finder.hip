@@ -12,7 +12,7 @@
 //   k_found_collect found(p) = admitted(p) && all first[bit_i(p)] < order(p)
 //                   -- exactly "all bits were set by an earlier window";
 //                   collected(p) = found(p) && !(similar && found(p-1));
-//                   wave-ballot compaction of collected hashes
+//                   workgroup compaction of collected hashes (one atomic per WG)
 //   sort + unique   H = sorted unique collected hashes (rocPRIM radix sort)
 //   k_table_insert  open-addressing table hash -> index in H
 //   k_ff_count      count[idx(h)]++ for every valid window whose hash is in H
@@ -180,51 +180,28 @@ __device__ __forceinline__ bool found_at(const AfArgs& a, const SeqMeta& s, int6
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(WG) void k_bloom_first(AfArgs a, uint32_t* __restrict__ first) {
-    const Chunk c = a.chunks[blockIdx.x];
-    const SeqMeta s = a.meta[c.seq];
-    const int64_t p = c.pos + threadIdx.x;
-    uint64_t h, dir;
-    if (!admitted(a, s, p, h, dir)) return;
-    const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
-    for (int i = 0; i < a.kb; i++) {
-        const uint32_t idx = bloom_index(h ^ a.params[i], a.m, a.mmagic);
-        atomicMin(&first[idx], ord);
-    }
-}
-
-__global__ __launch_bounds__(WG) void k_found_collect(AfArgs a, const uint32_t* __restrict__ first,
-                                                      uint64_t* __restrict__ out,
-                                                      unsigned long long* __restrict__ n_out) {
-    __shared__ uint8_t fs[WG];
-    const Chunk c = a.chunks[blockIdx.x];
-    const SeqMeta s = a.meta[c.seq];
-    const int t = threadIdx.x;
-    const int64_t p = c.pos + t;
-    uint64_t h = 0;
-    const bool f = found_at(a, s, p, first, h);
-    fs[t] = f;
-    __syncthreads();
-    bool prev;
-    if (t > 0) {
-        prev = fs[t - 1];
-    } else {
-        uint64_t hp;
-        prev = found_at(a, s, p - 1, first, hp);  // p-1 < 0 -> false (AnchorFinder.cpp:189)
-    }
-    const bool col = f && !(a.similar && prev);
-    // wave-aggregated append
+// Appends h to out for every thread with col set, one atomic on the shared
+// counter per workgroup: with one per wave the counter's serialized atomics
+// bounded found/collect (most waves collect a window)
+__device__ __forceinline__ void wg_append(bool col, uint64_t h, uint64_t* __restrict__ out,
+                                          unsigned long long* __restrict__ n_out) {
+    __shared__ uint32_t wcnt[WG / 64];
+    __shared__ unsigned long long wbase;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const unsigned long long mask = __ballot(col);
-    if (mask == 0) return;
-    const int lane = t & 63;
-    const int leader = __ffsll((long long)mask) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(n_out, (unsigned long long)__popcll(mask));
-    base = __shfl(base, leader);
-    if (col) {
-        const unsigned long long below = mask & ((1ull << lane) - 1ull);
-        out[base + __popcll(below)] = h;
+    if (lane == 0) wcnt[wv] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t tot = 0;
+        for (int i = 0; i < WG / 64; i++) {
+            const uint32_t c = wcnt[i];
+            wcnt[i] = tot;
+            tot += c;
+        }
+        wbase = tot ? atomicAdd(n_out, (unsigned long long)tot) : 0ull;
     }
+    __syncthreads();
+    if (col) out[wbase + wcnt[wv] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = h;
 }
 
 // ---- epoch-filtered Bloom pass (one GPU).  The windows run in epochs of
@@ -368,17 +345,7 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
         const int64_t last = min((int64_t)WG, s.size - a.k + 1 - c.pos) - 1;
         if (t == last) blast[0] = f ? 1ull : 0ull;
     }
-    const unsigned long long mask = __ballot(col);
-    if (mask == 0) return;
-    const int lane = t & 63;
-    const int leader = __ffsll((long long)mask) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(n_out, (unsigned long long)__popcll(mask));
-    base = __shfl(base, leader);
-    if (col) {
-        const unsigned long long below = mask & ((1ull << lane) - 1ull);
-        out[base + __popcll(below)] = h;
-    }
+    wg_append(col, h, out, n_out);
 }
 
 // this rank's Bloom bit array: the bits its admitted windows set

@@ -21,6 +21,12 @@ cut -c1-600 $O/bench_c3.json
 step bench_c2
 timeout -k 10 600 python bench.py --config C2 --steps 20 --warmup 5 --cpu-runs 3 > $O/bench_c2.json 2> $O/bench_c2.err || { tail -5 $O/bench_c2.err; exit 1; }
 cut -c1-300 $O/bench_c2.json
+step bench_c3_loop
+timeout -k 10 600 python bench.py --anchor-loop --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_c3_loop.json 2> $O/bench_c3_loop.err || { tail -5 $O/bench_c3_loop.err; exit 1; }
+cut -c1-300 $O/bench_c3_loop.json
+step bench_c4
+timeout -k 10 600 python bench.py --config C4 --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_c4.json 2> $O/bench_c4.err || { tail -5 $O/bench_c4.err; exit 1; }
+cut -c1-300 $O/bench_c4.json
 [ "$2" = quick ] && { step done; exit 0; }
 step rocprof_c3
 cd /tmp

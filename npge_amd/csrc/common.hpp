@@ -204,34 +204,6 @@ struct StageTimer {
 
 int current_device_checked();
 
-// f(i) for i < n; with at least 2^20 units of work in all, on up to
-// OMP_NUM_THREADS (else 16) host threads, each taking the next index
-inline void heavy_for(size_t n, int64_t work, const std::function<void(size_t)>& f) {
-    int cap = 16;
-    if (const char* e = getenv("OMP_NUM_THREADS")) cap = std::max(1, atoi(e));
-    const int T = (int)std::min<size_t>(n, (size_t)std::min<unsigned>(cap, std::max(1u, std::thread::hardware_concurrency())));
-    if (work < (1 << 20) || T <= 1) {
-        for (size_t i = 0; i < n; i++) f(i);
-        return;
-    }
-    std::atomic<size_t> next{0};
-    std::exception_ptr err;
-    std::mutex m;
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++)
-        th.emplace_back([&] {
-            try {
-                for (size_t i; (i = next++) < n;) f(i);
-            } catch (...) {
-                std::lock_guard<std::mutex> g(m);
-                if (!err) err = std::current_exception();
-            }
-        });
-    for (auto& x : th) x.join();
-    if (err) std::rethrow_exception(err);
-}
-
-
 // Small persistent host thread pool for the block bookkeeping that is
 // independent per block (hashing).  run(n, f) calls f(i) for i < n on the
 // workers and the calling thread and returns when all are done.
@@ -256,6 +228,11 @@ class HostPool {
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
+
+// f(i) for i < n; with at least 2^20 units of work in all, on a persistent
+// pool of up to OMP_NUM_THREADS (else 16) host threads (seqset.hip), each
+// taking the next index; the first exception is rethrown
+void heavy_for(size_t n, int64_t work, const std::function<void(size_t)>& f);
 
 // similar_aligner.hip: batched align_seqs (results in the aligner's host buffers)
 void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,

@@ -110,6 +110,34 @@ __global__ void k_pack(const unsigned char* __restrict__ ascii, const int64_t* _
 
 namespace npgx {
 
+void heavy_for(size_t n, int64_t work, const std::function<void(size_t)>& f) {
+    static HostPool* pool = [] {
+        int cap = 16;
+        if (const char* e = getenv("OMP_NUM_THREADS")) cap = std::max(1, atoi(e));
+        return new HostPool(std::min<int>(cap, (int)std::max(1u, std::thread::hardware_concurrency())));
+    }();
+    static std::mutex busy;
+    std::unique_lock<std::mutex> lk(busy, std::try_to_lock);
+    if (work < (1 << 20) || n < 2 || pool->size() < 2 || !lk.owns_lock()) {  // small, or the pool is in use
+        for (size_t i = 0; i < n; i++) f(i);
+        return;
+    }
+    std::exception_ptr err;
+    std::mutex m;
+    std::atomic<bool> failed{false};
+    pool->run(n, [&](size_t i) {
+        if (failed.load(std::memory_order_relaxed)) return;
+        try {
+            f(i);
+        } catch (...) {
+            std::lock_guard<std::mutex> g(m);
+            if (!err) err = std::current_exception();
+            failed = true;
+        }
+    });
+    if (err) std::rethrow_exception(err);
+}
+
 hipError_t stream_wait(hipStream_t s) {
     hipError_t e;
     while ((e = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
@@ -211,7 +239,7 @@ void HostPool::loop() {
 }
 
 void HostPool::run(size_t n, const std::function<void(size_t)>& f) {
-    if (workers_.empty() || n < 64) {
+    if (workers_.empty() || n < 2) {
         for (size_t i = 0; i < n; i++) f(i);
         return;
     }

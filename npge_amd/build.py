@@ -14,7 +14,7 @@ LIB = os.path.join(HERE, "libnpge_amd.so")
 # (loaded by _capi when NPGX_PROFILE=1)
 LIB_PROF = os.path.join(HERE, "libnpge_amd_prof.so")
 SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip", "block_build.hip",
-           "general_aligner.hip", "host_sampler.cpp"]
+           "general_aligner.hip", "wide_aligner.hip", "host_sampler.cpp"]
 HEADERS = ["common.hpp", "sa_device.hpp", "log_score.inc"]
 ARCH = os.environ.get("NPGX_OFFLOAD_ARCH", "gfx950")
 

@@ -247,6 +247,18 @@ struct AlignResult {
 };
 void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, const int32_t* row_len,
                   const int32_t* job_row_start, int32_t n_jobs, AlignResult& res);
+// wide_aligner.hip: align_seqs for problems of more than 64 non-empty rows (one
+// workgroup per problem); results stay in the WideBufs (row r at ptr + r * cap)
+struct WideJobIn {
+    int64_t row0;  // first of the problem's non-empty rows in ne_off / ne_len
+    int32_t n, pad;
+};
+struct WideBufs;
+WideBufs* wide_create();
+void wide_free(WideBufs* w);
+void align_wide(WideBufs* w, hipStream_t st, const char* d_rows, const int64_t* ne_off, const int32_t* ne_len,
+                int64_t n_ne, const std::vector<WideJobIn>& in, const int params[5], int aligner_type,
+                std::vector<int32_t>& len, std::vector<int32_t>& cap, std::vector<const char*>& ptr);
 void aligner_timer_reset(npgx_aligner* al);
 const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al);
 void aligner_host_ms(npgx_aligner* al, double* prep, double* wait);  // read and clear

@@ -2334,6 +2334,7 @@ struct npgx_aligner {
     bool has_result = false;
     bool want_stats = false;  // per-job statistics copied back (NPGX_JOB_STATS=1)
     StageTimer timer;
+    WideBufs* wide = nullptr;  // problems of more than 64 rows (wide_aligner.hip)
 };
 
 namespace npgx {
@@ -2369,6 +2370,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     jmax.resize(n_jobs);
     int64_t scratch = 0, n_reg = 0, n_sub_max = 0;
     int max_n = 1, max_len = 1, max_cap = 1;
+    std::vector<WideJobIn> wide_in;
+    std::vector<int32_t> wide_idx;
     const int wf = weight_factor(o.min_identity_x1e4);
     // after reduce_regions every region but a lone one weighs >= min_length:
     // at least this many columns wide
@@ -2392,8 +2395,20 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             sum += len;
             mx = std::max<int>(mx, (int)len);
         }
-        NPGX_REQUIRE(n <= 64, NPGX_ERR_RANGE, "more than 64 non-empty rows in one alignment");
         J.n = n;
+        if (n > 64) {  // a wide problem: one workgroup of its own (wide_aligner.hip)
+            wide_in.push_back(WideJobIn{J.row0, n, 0});
+            wide_idx.push_back(j);
+            J.cap = 0;
+            J.scratch = 0;
+            J.reg_off = 0;
+            J.reg_cap = 0;
+            J.pad = 0;
+            cost[j] = 0;
+            jsum[j] = (int32_t)std::min<int64_t>(sum, INT32_MAX);
+            jmax[j] = mx;
+            continue;
+        }
         // first attempt: 2*max+64 columns (the proven bound is the sum of lengths)
         int64_t cap = std::min<int64_t>(sum, 2ll * mx + 64);
         if (o.aligner_type == 1) cap = mx;
@@ -2441,6 +2456,12 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             acc += cnt[c];
         }
         for (int32_t j = 0; j < n_jobs; j++) order[at[cls[j]]++] = j;
+        if (!wide_idx.empty()) {  // the wide problems are not in the batched queue
+            std::vector<uint8_t> is_wide(n_jobs, 0);
+            for (int32_t j : wide_idx) is_wide[j] = 1;
+            order.erase(std::remove_if(order.begin(), order.end(), [&](int32_t j) { return is_wide[j] != 0; }),
+                        order.end());
+        }
     }
 
     pmark(1);
@@ -3041,6 +3062,21 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             throw Error(NPGX_ERR_RANGE, "alignment exceeded the proven column bound");
         todo.swap(again);
     }
+    if (!wide_idx.empty()) {
+        if (!al->wide) al->wide = wide_create();
+        const int params[5] = {o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
+        std::vector<int32_t> wl, wc;
+        std::vector<const char*> wp;
+        auto ti = al->timer.begin("align_wide", st, 0.0, 0);
+        align_wide(al->wide, st, d_rows, ne_off.data(), ne_len.data(), (int64_t)ne_len.size(), wide_in, params,
+                   o.aligner_type, wl, wc, wp);
+        al->timer.end(ti, st);
+        for (size_t q = 0; q < wide_idx.size(); q++) {
+            res.len[wide_idx[q]] = wl[q];
+            res.cap[wide_idx[q]] = wc[q];
+            res.bptr[wide_idx[q]] = wp[q];
+        }
+    }
     al->host_ms[0] += ms(tp);
     pmark(10);
     if (pdbg)
@@ -3243,6 +3279,7 @@ void npgx_aligner_free(npgx_aligner* a) {
     if (!a) return;
     (void)hipSetDevice(a->device);
     if (a->stream) (void)hipStreamDestroy(a->stream);
+    wide_free(a->wide);
     delete a;
 }
 

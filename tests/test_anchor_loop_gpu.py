@@ -97,9 +97,10 @@ def test_fragments_extender_portion_option():
         assert canon(eng.blocks()) == canon(ref.blocks())
 
 
-def _repeat_genomes(copies, genomes=2, unit=300, seed=5):
+def _repeat_genomes(copies, genomes=2, unit=300, seed=5, where=None):
     """Genomes of random sequence with `copies` slightly mutated copies of one
-    repeat unit each (an IS-element-like family)."""
+    repeat unit each (an IS-element-like family); `where` collects the copies
+    as fragments (genome, first, last, ori)."""
     import numpy as np
     rng = np.random.default_rng(seed)
     rep = rng.integers(0, 4, unit)
@@ -108,6 +109,9 @@ def _repeat_genomes(copies, genomes=2, unit=300, seed=5):
         parts = []
         for _ in range(copies):
             parts.append(rng.integers(0, 4, int(rng.integers(200, 400))))
+            if where is not None:
+                at = sum(len(p) for p in parts)
+                where.append((g, at, at + unit - 1, 1 if len(where) % 3 else -1, None))
             r = rep.copy()
             m = rng.random(unit) < 0.01
             r[m] = (r[m] + rng.integers(1, 4, int(m.sum()))) % 4
@@ -118,26 +122,41 @@ def _repeat_genomes(copies, genomes=2, unit=300, seed=5):
     return names, seqs
 
 
-def test_more_than_64_rows_fail_loudly():
-    """The aligner's lanes are rows: a block of more than 64 fragments (a
-    repeat family across genomes) is refused with NPGX_ERR_RANGE instead of
-    being cut -- MetaAligner on such a block and AnchorLoopFast on genomes
-    carrying 40 copies each (80-fragment anchors).  With 30 copies per genome
-    (60 fragments) the same pipe runs and matches the oracle."""
-    from npge_amd import _capi
+def test_more_than_64_rows():
+    """A block of more than 64 fragments (a repeat family across genomes) is
+    aligned by the workgroup-per-problem aligner (wide_aligner.hip):
+    AnchorLoopFast (FragmentsExtender flanks and the closing Align of
+    80-fragment blocks) on genomes carrying 40 copies each, and 30 copies (60
+    fragments, the batched aligner), both matching the oracle."""
     from npge_amd.anchor_finder import AnchorFinder
     from npge_amd.anchor_loop import anchor_loop_fast
-    names, seqs = _repeat_genomes(40)
-    eng = _engine(seqs, names, [])
-    with pytest.raises(_capi.NpgxError) as e:
-        anchor_loop_fast(eng, AnchorFinder())
-    assert e.value.code == -4 and "64" in str(e.value)
-    names, seqs = _repeat_genomes(30)
-    eng = _engine(seqs, names, [])
-    st = anchor_loop_fast(eng, AnchorFinder())
+    for copies in (40, 30):
+        names, seqs = _repeat_genomes(copies)
+        eng = _engine(seqs, names, [])
+        st = anchor_loop_fast(eng, AnchorFinder())
+        o = orc.BlockSetOracle(seqs, names)
+        o.set_blocks([])
+        ost = _oracle_loop(o)
+        assert st["anchors"] > 0
+        assert st["loop_iterations"] == ost["iterations"]
+        assert canon(eng.blocks()) == canon(o.blocks())
+
+
+def test_align_more_than_64_fragments():
+    """MetaAligner (Align) on a block of 80 unaligned repeat copies (mixed
+    orientations, widened by random amounts) next to ordinary blocks: rows
+    bit-exact vs the oracle's align_block + refine_alignment."""
+    import numpy as np
+    where = []
+    names, seqs = _repeat_genomes(40, where=where)
+    rng = np.random.default_rng(8)
+    wide = [(g, max(0, a - int(rng.integers(0, 30))), min(len(seqs[g]) - 1, b + int(rng.integers(0, 30))), o, None)
+            for g, a, b, o, _ in where]
+    blocks = [wide, wide[:3], wide[10:75]]
+    eng = _engine(seqs, names, blocks).apply("Align")
     o = orc.BlockSetOracle(seqs, names)
-    o.set_blocks([])
-    ost = _oracle_loop(o)
-    assert st["anchors"] > 0
-    assert st["loop_iterations"] == ost["iterations"]
-    assert canon(eng.blocks()) == canon(o.blocks())
+    o.set_blocks(blocks)
+    o.apply("MetaAligner")
+    got = eng.blocks()
+    assert got == o.blocks()
+    assert max(len(b) for b in got) == 80 and any("-" in (f[4] or "") for b in got for f in b)

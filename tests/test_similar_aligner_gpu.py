@@ -207,10 +207,26 @@ def test_dummy_random():
     _check(_random_jobs(5, 50), kind="dummy")
 
 
-def test_too_many_rows_rejected():
-    from npge_amd import _capi
-    with pytest.raises(_capi.NpgxError):
-        _aligner().align([["ACGT"] * 65])
+def test_more_than_64_rows():
+    """Problems of more than 64 non-empty rows go to the workgroup-per-problem
+    aligner (wide_aligner.hip): repeat-family-like mutated copies, unrelated
+    tails, N runs, empty rows, next to narrow jobs in the same batch."""
+    rng = np.random.default_rng(65)
+    jobs = [["ACGT"] * 65, ["ACGT"] * 64 + ["ACGA"], [""] * 10 + ["AC"] * 70]
+    for n, L, d in ((65, 40, 0.02), (80, 300, 0.01), (100, 200, 0.05), (130, 150, 0.15), (70, 500, 0.005),
+                    (300, 120, 0.03), (66, 250, 0.4)):
+        jobs.append(_family(rng, n, L, d, tail_unrelated=0.3, nrate=0.05))
+    jobs.append(_family(rng, 5, 100, 0.05))  # a narrow job in the same batch
+    _check(jobs)
+    _check(jobs, kind="dummy")
+
+
+def test_more_than_64_rows_random():
+    rng = np.random.default_rng(99)
+    jobs = [_family(rng, int(rng.integers(65, 200)), int(rng.integers(1, 400)),
+                    float(rng.choice([0.0, 0.01, 0.05, 0.2])), tail_unrelated=float(rng.choice([0.0, 0.5])))
+            for _ in range(12)]
+    _check(jobs)
 
 
 @pytest.mark.parametrize("cfg", ["tiny", "small"])

@@ -480,6 +480,8 @@ struct npgx_af {
     std::vector<SeqMeta> layout_meta;  // d_meta / d_chunks hold this layout (chunks follow from it and k)
     int layout_k = 0;
     int64_t layout_n = -1;
+    std::vector<Chunk> layout_chunks;  // host copy of d_chunks
+    int64_t layout_c0 = -1, layout_c1 = -1, layout_local = 0;  // this rank's chunk range and its windows
     DevBuf<Chunk> d_chunks;
     DevBuf<uint32_t> first;
     DevBuf<uint32_t> bloom_bits;  // P of the epoch-filtered pass
@@ -616,16 +618,23 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     int32_t R = 0;
     while (R < ss->n && (int64_t)ss->data[ss->by_rank[R]].size() >= k) R++;
     std::vector<SeqMeta> meta(R > 0 ? R : 1);
-    std::vector<Chunk> chunks;
     uint64_t order = 0;
     int64_t n_windows = 0;
     for (int32_t r = 0; r < R; r++) {
         const int64_t size = (int64_t)ss->data[ss->by_rank[r]].size();
         meta[r] = SeqMeta{size, ss->word_off[r], ss->n_off[r], order};
         order += (uint64_t)size;
-        const int64_t nw = size - k + 1;
-        n_windows += nw;
-        for (int64_t p = 0; p < nw; p += WG) chunks.push_back(Chunk{r, 0, p});
+        n_windows += size - k + 1;
+    }
+    // the window layout depends only on the sequence set and k: built and
+    // uploaded once per (set, k) and reused by later runs of this handle
+    const bool same_layout = af->layout_k == k && af->layout_meta.size() == meta.size() &&
+                             memcmp(af->layout_meta.data(), meta.data(), meta.size() * sizeof(SeqMeta)) == 0;
+    std::vector<Chunk>& chunks = af->layout_chunks;
+    if (!same_layout) {
+        chunks.clear();
+        for (int32_t r = 0; r < R; r++)
+            for (int64_t p = 0; p < meta[r].size - k + 1; p += WG) chunks.push_back(Chunk{r, 0, p});
     }
     NPGX_REQUIRE(order < 0xFFFFFFFEull, NPGX_ERR_RANGE, "more than 2^32-2 bases in one run");
     S.n_windows = n_windows;
@@ -647,9 +656,14 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     const int64_t nchunks = c1 - c0;
     if (comm) NPGX_REQUIRE(n_windows < (1ll << 31), NPGX_ERR_RANGE,
                            "sharded run: FoundFragment counts must fit int32");
-    int64_t local_windows = 0;
-    for (int64_t c = c0; c < c1; c++)
-        local_windows += std::min<int64_t>(WG, meta[chunks[c].seq].size - k + 1 - chunks[c].pos);
+    if (!same_layout || af->layout_c0 != c0 || af->layout_c1 != c1) {
+        int64_t lw = 0;
+        for (int64_t c = c0; c < c1; c++) lw += std::min<int64_t>(WG, meta[chunks[c].seq].size - k + 1 - chunks[c].pos);
+        af->layout_local = lw;
+        af->layout_c0 = c0;
+        af->layout_c1 = c1;
+    }
+    const int64_t local_windows = af->layout_local;
     if (nchunks_all == 0) {
         af->r_block_start.assign(1, 0);
         af->r_seq.clear();
@@ -659,11 +673,6 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         af->has_result = true;
         return;
     }
-    // the window layout depends only on the sequence set and k: uploaded once
-    // per (set, k) and reused by later runs of this handle
-    const bool same_layout = af->layout_k == k && af->layout_n == (int64_t)chunks.size() &&
-                             af->layout_meta.size() == meta.size() &&
-                             memcmp(af->layout_meta.data(), meta.data(), meta.size() * sizeof(SeqMeta)) == 0;
     if (!same_layout) {
         af->d_meta.ensure(meta.size());
         af->d_chunks.ensure(chunks.size());

@@ -35,6 +35,8 @@
 #include <cstring>
 #include <map>
 
+#include <chrono>
+
 #include "common.hpp"
 
 namespace npgx {
@@ -505,6 +507,7 @@ struct npgx_af {
     std::vector<int8_t> r_ori;
     StageTimer timer;
     std::vector<uint64_t> host_keys, host_H;
+    std::vector<size_t> h_group_key;  // grouping: first key of each kept group
 
     void ensure_temp(size_t bytes) { temp.ensure(bytes); }
 };
@@ -583,6 +586,10 @@ static void comm_check(int rc, const char* what) {
 }
 
 static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
+    static const bool hdbg = getenv("NPGX_AF_DEBUG") != nullptr;  // host phase times to stderr
+    const auto th0 = std::chrono::steady_clock::now();
+    auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count(); };
+    double h_prep = 0, h_dl = 0;
     NPGX_REQUIRE(ss->device == af->device, NPGX_ERR_ARG, "sequence set and finder on different devices");
     NPGX_HIP(hipSetDevice(af->device));
     hipStream_t st = af->stream;
@@ -701,6 +708,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     A.similar = af->opt.anchor_similar ? 1 : 0;
 
     const dim3 grid((unsigned)std::max<int64_t>(nchunks, 1)), block(WG);
+    h_prep = hms();
     const bool run_local = nchunks > 0;  // ranks without windows still join every collective
     uint64_t* hp = af->h_pinned;
 
@@ -981,49 +989,70 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         }
     }
 
+    h_dl = hms();
     // --- fragmenttg_postprocess (AnchorFinder.cpp:356-391) on the truncated list
     std::vector<uint64_t> prefix2(R);
     for (int32_t r = 0; r < R; r++) prefix2[r] = 2ull * meta[r].order_off;
     const uint64_t key_mask = key_bits >= 64 ? ~0ull : ((1ull << key_bits) - 1);
-    af->r_block_start.clear();
-    af->r_seq.clear();
-    af->r_min.clear();
-    af->r_max.clear();
-    af->r_ori.clear();
     const bool sort_used = !af->used.empty();
-    size_t i = 0;
+    // pass 1 (sequential, cheap): the groups, the used-hash quirk and the
+    // output offsets of the groups of two or more fragments
+    const size_t nk = keys.size();
+    std::vector<size_t>& gk = af->h_group_key;  // first key of each kept group
+    gk.clear();
+    af->r_block_start.clear();
+    int64_t nout = 0;
     bool first_group = true;
-    while (i < keys.size()) {
+    for (size_t i = 0; i < nk;) {
         const uint64_t idx = keys[i] >> key_bits;
         size_t j = i + 1;
-        while (j < keys.size() && (keys[j] >> key_bits) == idx) j++;
+        while (j < nk && (keys[j] >> key_bits) == idx) j++;
         if (!first_group) af->used.push_back(Hh[idx]);  // quirk: not the first group
         first_group = false;
         if (j - i >= 2) {
-            af->r_block_start.push_back((int64_t)af->r_seq.size());
-            for (size_t q = i; q < j; q++) {
-                const uint64_t key2 = keys[q] & key_mask;
-                const int32_t r = (int32_t)(std::upper_bound(prefix2.begin(), prefix2.end(), key2) -
-                                            prefix2.begin()) - 1;
-                const uint64_t pos2 = key2 - prefix2[r];
-                const uint64_t size = (uint64_t)meta[r].size;
-                const bool direct = pos2 < size;   // FoundFragment::make_fragment :240-246
-                const int64_t mn = (int64_t)(direct ? pos2 : pos2 - size);
-                af->r_seq.push_back(ss->by_rank[r]);
-                af->r_min.push_back(mn);
-                af->r_max.push_back(mn + k - 1);
-                af->r_ori.push_back(direct ? 1 : -1);
-            }
+            af->r_block_start.push_back(nout);
+            gk.push_back(i);
+            nout += (int64_t)(j - i);
         }
         i = j;
     }
-    af->r_block_start.push_back((int64_t)af->r_seq.size());
+    af->r_block_start.push_back(nout);
+    af->r_seq.resize((size_t)nout);
+    af->r_min.resize((size_t)nout);
+    af->r_max.resize((size_t)nout);
+    af->r_ori.resize((size_t)nout);
+    // pass 2: the fragments (FoundFragment::make_fragment :240-246), groups on
+    // host threads; a group's keys ascend, so its sequence rank only moves forward
+    const double h_pass1 = hms();
+    const size_t ng = gk.size(), per = 256;  // groups per task: few tasks on the pool's shared counter
+    heavy_for((ng + per - 1) / per, nout * 16, [&](size_t t) {
+      for (size_t g = t * per; g < std::min(ng, (t + 1) * per); g++) {
+        size_t q = gk[g];
+        int32_t r = 0;
+        for (int64_t o = af->r_block_start[g]; o < af->r_block_start[g + 1]; o++, q++) {
+            const uint64_t key2 = keys[q] & key_mask;
+            if (r + 1 < R && prefix2[(size_t)r + 1] <= key2)
+                r = (int32_t)(std::upper_bound(prefix2.begin() + r + 1, prefix2.end(), key2) - prefix2.begin()) - 1;
+            const uint64_t pos2 = key2 - prefix2[(size_t)r];
+            const uint64_t size = (uint64_t)meta[(size_t)r].size;
+            const bool direct = pos2 < size;
+            const int64_t mn = (int64_t)(direct ? pos2 : pos2 - size);
+            af->r_seq[(size_t)o] = ss->by_rank[(size_t)r];
+            af->r_min[(size_t)o] = mn;
+            af->r_max[(size_t)o] = mn + k - 1;
+            af->r_ori[(size_t)o] = direct ? 1 : -1;
+        }
+      }
+    });
     if (sort_used) std::sort(af->used.begin(), af->used.end());
     if (af->used.size() != (size_t)S.n_used) af->used_dirty = true;
     S.n_blocks = (int64_t)af->r_block_start.size() - 1;
     S.n_fragments = (int64_t)af->r_seq.size();
     S.n_used = (int64_t)af->used.size();
     af->has_result = true;
+    if (hdbg)
+        fprintf(stderr, "af host: prep %.3f ms, results downloaded at %.3f ms, grouping %.3f ms (groups %.3f ms; "
+                "%zu keys, %lld blocks)\n", h_prep, h_dl, hms() - h_dl, h_pass1 - h_dl, keys.size(), (long long)S.n_blocks);
 }
 
 }  // namespace npgx

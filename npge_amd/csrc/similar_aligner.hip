@@ -2234,6 +2234,29 @@ __global__ void k_gather_rows(const GatherRow* rows, int64_t n, char* out) {
     }
 }
 
+// A batch's small host->device arrays and zeroed counters in one upload: the
+// arrays are staged back to back after a table of these ops, copied in one
+// hipMemcpy and scattered by one launch (instead of ~10 copies and 4 fills,
+// each a serialized dispatch of ~8 us, per aligner batch)
+struct ScatterOp {
+    void* dst;
+    int64_t src;    // byte offset in the blob; < 0: zero fill
+    int64_t bytes;
+};
+
+__global__ void k_scatter(const unsigned char* __restrict__ blob, int n_ops) {
+    const ScatterOp op = ((const ScatterOp*)blob)[blockIdx.x];
+    const int64_t t = (int64_t)blockIdx.y * blockDim.x + threadIdx.x, step = (int64_t)gridDim.y * blockDim.x;
+    if (op.bytes % 4 == 0 && ((uintptr_t)op.dst & 3) == 0) {
+        uint32_t* d = (uint32_t*)op.dst;
+        const uint32_t* sp = (const uint32_t*)(blob + (op.src < 0 ? 0 : op.src));
+        for (int64_t i = t; i < op.bytes / 4; i += step) d[i] = op.src < 0 ? 0u : sp[i];
+    } else {
+        unsigned char* d = (unsigned char*)op.dst;
+        for (int64_t i = t; i < op.bytes; i += step) d[i] = op.src < 0 ? 0 : blob[op.src + i];
+    }
+}
+
 int weight_factor(int64_t min_identity_x1e4) {
     // FindLowSimilar::get_weight_factor with Decimal arithmetic (Decimal.hpp)
     int64_t mi = std::min<int64_t>(min_identity_x1e4, 9900);
@@ -2335,6 +2358,10 @@ struct npgx_aligner {
     bool want_stats = false;  // per-job statistics copied back (NPGX_JOB_STATS=1)
     StageTimer timer;
     WideBufs* wide = nullptr;  // problems of more than 64 rows (wide_aligner.hip)
+    // the batch's small uploads and zeroed counters, scattered by one launch
+    std::vector<npgx::ScatterOp> h_ops;
+    std::vector<unsigned char> h_blob;
+    DevBuf<unsigned char> d_blob;
 };
 
 namespace npgx {
@@ -2474,11 +2501,33 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     al->d_job_stats.ensure(jobs.size() * NPGX_JOB_STATS);
     al->job_stats.assign(al->want_stats ? jobs.size() * NPGX_JOB_STATS : 0, 0);
     al->d_next.ensure(1);
-    auto put = [&](void* d, const void* h, size_t bytes) {  // through pinned staging
+    // uploads and zeroings are collected and issued together by flush() before
+    // the next launch (one copy + one k_scatter)
+    al->h_ops.clear();
+    al->h_blob.clear();
+    auto put = [&](void* d, const void* h, size_t bytes) {
         if (!bytes) return;
-        char* p = al->pinned.take(bytes, st);
-        memcpy(p, h, bytes);
-        NPGX_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, st));
+        const size_t at = (al->h_blob.size() + 15) & ~(size_t)15;
+        al->h_blob.resize(at + bytes);
+        memcpy(al->h_blob.data() + at, h, bytes);
+        al->h_ops.push_back(ScatterOp{d, (int64_t)at, (int64_t)bytes});
+    };
+    auto zero = [&](void* d, size_t bytes) { al->h_ops.push_back(ScatterOp{d, -1, (int64_t)bytes}); };
+    auto flush = [&]() {
+        if (al->h_ops.empty()) return;
+        const size_t nop = al->h_ops.size(), head = (nop * sizeof(ScatterOp) + 15) & ~(size_t)15;
+        for (ScatterOp& op : al->h_ops)
+            if (op.src >= 0) op.src += (int64_t)head;
+        const size_t total = head + al->h_blob.size();
+        char* p = al->pinned.take(total, st);
+        memcpy(p, al->h_ops.data(), nop * sizeof(ScatterOp));
+        memcpy(p + head, al->h_blob.data(), al->h_blob.size());
+        al->d_blob.ensure(total);
+        NPGX_HIP(hipMemcpyAsync(al->d_blob.p, p, total, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_scatter, dim3((unsigned)nop, 16), dim3(256), 0, st, al->d_blob.p, (int)nop);
+        NPGX_HIP(hipGetLastError());
+        al->h_ops.clear();
+        al->h_blob.clear();
     };
     put(al->d_row_off.p, ne_off.data(), ne_off.size() * 8);
     put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
@@ -2584,7 +2633,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         put(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob));
         al->d_order.grow(queue.size());
         put(al->d_order.p, queue.data(), queue.size() * 4);
-        NPGX_HIP(hipMemsetAsync(al->d_next.p, 0, 4, st));
+        zero(al->d_next.p, 4);
         pmark(3);
         // per-slot scratch: the word table (20 B an entry), the append_aligned
         // stack (1028 B a level) and the regions of unsplit jobs (17 B a
@@ -2627,7 +2676,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             al->epoch_base = 1;
         }
         al->slot_epoch.ensure(1);
-        NPGX_HIP(hipMemsetAsync(al->slot_epoch.p, 0, 4, st));
+        zero(al->slot_epoch.p, 4);
         al->st_p.ensure(slots * depth * 64);
         al->st_len.ensure(slots * depth * 64);
         al->st_pos.ensure(slots * depth * 64);
@@ -2685,8 +2734,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             al->d_counters.ensure(4);
             // sub-job outputs: about what the jobs' own scratch holds
             al->d_pool.grow((size_t)scratch + (16u << 20));
-            NPGX_HIP(hipMemsetAsync(al->d_alloc.p, 0, 16, st));
-            NPGX_HIP(hipMemsetAsync(al->d_counters.p, 0, 16, st));
+            zero(al->d_alloc.p, 16);
+            zero(al->d_counters.p, 16);
             A.job_regions = al->d_job_regions.p;
             A.job_nreg = al->d_job_nreg.p;
             A.subs = al->d_subs.p;
@@ -2827,6 +2876,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A.qseg = al->d_qseg.p;
             A.qsub = al->d_qsub.p;
             A.ftasks = al->d_ftasks.p;
+            flush();
             if (n_job_find > 0) {
                 size_t tf = al->timer.begin("align_split", st, 0.0, (int64_t)n_job_find);
                 hipLaunchKernelGGL(k_split_find, dim3((unsigned)n_job_find), dim3(64 * SPLIT_WAVES), SPLIT_LDS, st, A,
@@ -2838,6 +2888,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         pmark(6);
         int64_t residues = 0;
         for (int32_t j : todo) residues += jsum[j];
+        flush();
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
                                     double(residues) * 2.0, residues);
         hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);

@@ -126,6 +126,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample or args.config, args.cpu_runs)
+        if args.anchor_loop:  # the CPU leg times DraftPangenome only: not like-for-like
+            cpu["workload"] = "DraftPangenome only (the GPU step adds AnchorLoopFast): no speedup ratio implied"
 
     if rank == 0:
         line = {
@@ -197,7 +199,7 @@ def _cpu_info():
 def cpu_baseline(config, runs=5):
     """The CPU restatement (oracle/) timed on this host on the same workload,
     built -O3 -march=native on this host (oracle/Makefile `native`): one thread
-    (reference 1-worker semantics) and, under "all_cores", with FragmentTG +
+    (reference 1-worker semantics) and, under "allotted_cores", with FragmentTG +
     BlocksJobs threading (the reference's --workers; the Bloom pass sequential)
     over every core this job is allotted.  Each is the median of `runs` timed
     runs after one warm-up (steady clock), input packing excluded like the GPU
@@ -240,12 +242,15 @@ def cpu_baseline(config, runs=5):
     if hn != h1:
         raise AssertionError("threaded oracle DraftPangenome differs from the 1-thread run")
     return {"value": round(bp / 1e6 / t1, 4), "unit": "Mbp/s", "cores": 1, "kind": "port",
-            "sample": "%s synthetic set (%d bp), one full DraftPangenome step of the same workload, "
+            "sample": "%s synthetic set (%d bp), one full DraftPangenome step, "
                       "oracle/ C++ %s, 1 thread, median of %d runs after 1 warm-up"
                       % (config, bp, "-O3 -march=native" if native else "-O3 (prebuilt)", runs),
+            "workload": "DraftPangenome",
             "seconds": round(t1, 3), "runs_s": [round(x, 3) for x in ts1],
             "host": info,
-            "all_cores": {"value": round(bp / 1e6 / tn, 4), "cores": workers, "seconds": round(tn, 3),
+            # the threads this job is allotted (OMP_NUM_THREADS, the box's per-GPU CPU share),
+            # not every core of the machine (host.affinity)
+            "allotted_cores": {"value": round(bp / 1e6 / tn, 4), "cores": workers, "seconds": round(tn, 3),
                           "runs_s": [round(x, 3) for x in tsn],
                           "threading": "FragmentTG per sequence (AnchorFinder pass 2), BlocksJobs per block "
                                        "(DummyAligner, FragmentsExtender, FixEnds, Filter); the Bloom pass "

@@ -217,6 +217,16 @@ int npgx_align_kernel_times(const npgx_aligner* a, npgx_kernel_time* out, int32_
 int npgx_align_job_stats(const npgx_aligner* a, int64_t* out, int64_t cap, int64_t* n);
 void npgx_aligner_free(npgx_aligner* a);
 
+/* refine_alignment (replaces refine_alignment(Strings&), src/algo/refine_alignment.cpp:
+ * 182-190, the step AbstractAligner::align_block runs after align_seqs) for a
+ * batch of alignments on the GPU: alignment j = rows [job_row_start[j],
+ * job_row_start[j+1]), row r = rows[row_off[r] .. row_off[r+1]), the rows of
+ * one alignment of equal length and consecutive in `rows`.  The refined rows
+ * go to out at the same offsets; only their first out_len[j] characters are
+ * valid (pure-gap columns are removed). */
+int npgx_refine_batch(const char* rows, const int64_t* row_off, const int32_t* job_row_start, int32_t n_jobs,
+                      char* out, int32_t* out_len);
+
 
 /* ------------------------------------------------------------------ block sets
  * A block set over a sequence set: blocks of fragments (sequence input index,
@@ -225,10 +235,25 @@ void npgx_aligner_free(npgx_aligner* a);
  *   "RemoveNonStem"      RemoveNonStem --exact (src/algo/RemoveNonStem.cpp:29-45)
  *   "DummyAligner"       AbstractAligner::align_block with DummyAligner
  *                        (AbstractAligner.cpp:51-69, DummyAligner.cpp:18-26)
- *   "MetaAligner"/"Align" align_block with aligner-type similar: the blocks
+ *   "MetaAligner"        align_block with aligner-type similar: the blocks
  *                        alignment_needed selects aligned on the GPU, then
  *                        refine_alignment (AbstractAligner.cpp:51-69,145-177,
  *                        refine_alignment.cpp:15-190)
+ *   "Align"              Align (src/algo/Align.cpp:36-52): MetaAligner,
+ *                        SelfOverlapsResolver, MetaAligner, then the loop
+ *                        {MoveGaps, CutGaps, Filter} until the block set repeats
+ *   "LiteAlign"          LiteAlign (Align.cpp:17-30): MetaAligner, then the
+ *                        loop {MoveGaps, CutGaps}
+ *   "MoveGaps"           MoveGaps (src/algo/MoveGaps.cpp:30-103); options
+ *                        --max-tail=N --max-tail-to-gap=D
+ *   "CutGaps"            CutGaps (src/algo/CutGaps.cpp:136-159); option
+ *                        --cut-strict=0|1
+ *   "SelfOverlapsResolver" fix_self_overlaps (src/algo/hit.cpp:68-91)
+ *   "Rest"               Rest target=X other=X (src/algo/Rest.cpp:40-77)
+ *   "OverlaplessUnion"   OverlaplessUnion --ou-move into an empty target
+ *                        (src/algo/OverlaplessUnion.cpp:54-80)
+ *   "AnchorLoopFast"     the AnchorLoopFast pipe (lua_lib.lua:741-758), af =
+ *                        its AnchorFinder
  *   "FragmentsExtender"  FragmentsExtender (src/algo/FragmentsExtender.cpp:87-119)
  *   "FixEnds"            FixEnds (src/algo/FixEnds.cpp:117-144)
  *   "ExtendLoopFast"     Pipe ExtendLoopFast (src/algo/lua_lib.lua:697-709,
@@ -241,7 +266,10 @@ typedef struct npgx_blockset npgx_blockset;
 typedef struct {
     int32_t extend_length;          /* FragmentsExtender extend-length (MIN_LENGTH 100) */
     int32_t max_iterations;         /* ExtendLoopFast iterations (DraftPangenome: 10) */
-    int64_t extend_portion_x1e4;    /* extend-length-portion (ExtendAndFix: 0.5) */
+    int64_t extend_portion_x1e4;    /* FragmentsExtender extend-length-portion: default 0
+                                     * (FragmentsExtender.cpp:28-30); ExtendAndFix /
+                                     * ExtendAndAlign (inside ExtendLoopFast, AnchorLoopFast)
+                                     * pass 0.5 themselves, whatever this holds */
     int32_t min_fragment;           /* FixEnds / Filter min-fragment (MIN_LENGTH) */
     int32_t frame_length;           /* Filter frame-length (FRAME_LENGTH 100) */
     int32_t min_end;                /* Filter min-end (MIN_END 10) */
@@ -250,6 +278,8 @@ typedef struct {
     int32_t find_subblocks;         /* Filter find-subblocks (1) */
     int64_t min_identity_x1e4;      /* FixEnds / Filter min-identity (MIN_IDENTITY 0.9) */
     npgx_align_options align;       /* aligner used by FragmentsExtender */
+    int32_t max_tail;               /* MoveGaps max-tail (MAX_TAIL 3) */
+    int64_t max_tail_to_gap_x1e4;   /* MoveGaps max-tail-to-gap (MAX_TAIL_TO_GAP 1.0) */
 } npgx_bb_options;
 
 typedef struct {

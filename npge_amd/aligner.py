@@ -15,6 +15,33 @@ from .processor import Decimal, Processor, register
 ALIGNER_TYPES = {"similar": 0, "dummy": 1}
 
 
+def refine_batch(alignments):
+    """refine_alignment (refine_alignment.cpp:182-190) of each alignment (a
+    list of equal-length gapped rows) on the GPU (npgx_refine_batch)."""
+    L = _capi.lib()
+    if not getattr(L, "_refine_bound", False):
+        vp = ctypes.c_void_p
+        L.npgx_refine_batch.argtypes = [vp, vp, vp, ctypes.c_int32, vp, vp]
+        L._refine_bound = True
+    rows = [r for a in alignments for r in a]
+    data = "".join(rows).encode()
+    off = np.zeros(len(rows) + 1, dtype=np.int64)
+    np.cumsum([len(r) for r in rows], out=off[1:])
+    jstart = np.zeros(len(alignments) + 1, dtype=np.int32)
+    np.cumsum([len(a) for a in alignments], out=jstart[1:])
+    buf = ctypes.create_string_buffer(data, max(len(data), 1))
+    out = ctypes.create_string_buffer(max(len(data), 1))
+    lens = np.zeros(max(len(alignments), 1), dtype=np.int32)
+    _capi.check(L.npgx_refine_batch(ctypes.cast(buf, ctypes.c_void_p), _capi.ptr(off), _capi.ptr(jstart),
+                                    len(alignments), ctypes.cast(out, ctypes.c_void_p), _capi.ptr(lens)))
+    raw = out.raw
+    res, k = [], 0
+    for j, a in enumerate(alignments):
+        res.append([raw[off[k + i]:off[k + i] + lens[j]].decode() for i in range(len(a))])
+        k += len(a)
+    return res
+
+
 class BatchAligner:
     """One npgx_aligner handle (one HIP stream)."""
 

@@ -1,8 +1,10 @@
 """Block-set processors on the engine (npgx_blockset_*).
 
 Mirrors the reference's BlockSet + per-block processors of the block build:
-RemoveNonStem, DummyAligner, FragmentsExtender, FixEnds, OverlaplessUnion,
-ExtendLoopFast, Filter and the DraftPangenome driver (lua_lib.lua:1569-1621).
+RemoveNonStem, DummyAligner, MetaAligner, FragmentsExtender, FixEnds,
+OverlaplessUnion, ExtendLoopFast, Filter, MoveGaps, CutGaps,
+SelfOverlapsResolver, the Align / LiteAlign pipes (Align.cpp:17-52), Rest,
+AnchorLoopFast and the DraftPangenome driver (lua_lib.lua:1569-1621).
 Alignment work goes to the HIP aligner in one batch per processor pass.
 """
 import ctypes
@@ -18,7 +20,8 @@ class BbOptions(ctypes.Structure):
                 ("frame_length", ctypes.c_int32), ("min_end", ctypes.c_int32),
                 ("min_block", ctypes.c_int32), ("max_block", ctypes.c_int32),
                 ("find_subblocks", ctypes.c_int32), ("min_identity_x1e4", ctypes.c_int64),
-                ("align", _capi.AlignOptions)]
+                ("align", _capi.AlignOptions), ("max_tail", ctypes.c_int32),
+                ("max_tail_to_gap_x1e4", ctypes.c_int64)]
 
 
 class BbStats(ctypes.Structure):

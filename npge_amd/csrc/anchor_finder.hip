@@ -643,7 +643,15 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         for (int32_t r = 0; r < R; r++)
             for (int64_t p = 0; p < meta[r].size - k + 1; p += WG) chunks.push_back(Chunk{r, 0, p});
     }
-    NPGX_REQUIRE(order < 0xFFFFFFFEull, NPGX_ERR_RANGE, "more than 2^32-2 bases in one run");
+    // window orders are 32-bit (first[] holds one per Bloom bit): a run over
+    // more bases is refused, never wrapped.  NPGX_AF_MAX_BASES lowers the
+    // limit (tests exercise the refusal without a 4 Gbp input).
+    static const uint64_t max_bases = [] {
+        const char* e = getenv("NPGX_AF_MAX_BASES");
+        const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+        return v > 0 && v < 0xFFFFFFFEull ? v : 0xFFFFFFFEull;
+    }();
+    NPGX_REQUIRE(order < max_bases, NPGX_ERR_RANGE, "more than 2^32-2 bases in one run (32-bit window orders)");
     S.n_windows = n_windows;
     S.n_used = (int64_t)af->used.size();
 

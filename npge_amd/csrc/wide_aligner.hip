@@ -28,6 +28,8 @@
 // MAXV gap variants is refused (NPGX_ERR_RANGE).
 #include <cstring>
 
+#include <deque>
+
 #include "common.hpp"
 
 namespace npgx {
@@ -48,7 +50,9 @@ struct WJob {
     int64_t out;           // byte offset of the n x cap output
     int64_t arena;         // byte offset of the job's arena
     int64_t arena_bytes;
+    int64_t tab;           // first entry of the job's pair / word tables (tcap = 1 << tlog2 each)
     int32_t n, cap;
+    uint32_t tlog2, pad;
 };
 
 struct WArgs {
@@ -62,7 +66,6 @@ struct WArgs {
     unsigned long long* wk;   // word table keys, tcap per job
     uint32_t* wc;             // word table counts
     uint32_t* used;           // used lists: pairs then words, tcap/2 each per job
-    uint32_t tcap_log2;
     int32_t* len_out;
     int32_t* status;          // 0 ok, 1 re-run larger, 2 refused
     int mc, gc, ac, min_length, wf, aligner_type;
@@ -158,7 +161,7 @@ struct Job {
     unsigned char* var;       // MAXV x n gap-variant offsets (0: pos, 1: pos + 1)
     unsigned long long *pt, *wk;
     uint32_t *wc, *pu, *wu;
-    uint32_t tcap;
+    uint32_t tcap, tlog2;
 
     // bump allocation from the arena (uniform: every thread computes the same)
     __device__ unsigned char* alloc(int64_t bytes) {
@@ -341,7 +344,7 @@ struct Job {
         __syncthreads();
     }
     __device__ uint32_t word_slot(unsigned long long w, bool insert) {
-        const uint32_t lg = a.tcap_log2, mask = tcap - 1;
+        const uint32_t lg = tlog2, mask = tcap - 1;
         uint32_t h = slot_of(w, lg);
         while (true) {
             unsigned long long k = aload(wk + h);
@@ -361,7 +364,7 @@ struct Job {
     }
     __device__ bool pair_insert(unsigned long long key) {  // true: new pair
         const uint32_t mask = tcap - 1;
-        uint32_t h = slot_of(key, a.tcap_log2);
+        uint32_t h = slot_of(key, tlog2);
         while (true) {
             const unsigned long long k = atomicCAS(pt + h, EMPTY, key);
             if (k == EMPTY) {
@@ -659,11 +662,12 @@ __global__ __launch_bounds__(WT) void k_align_wide(WArgs a) {
     J.arena = a.arena + W.arena;
     J.top = 0;
     J.lim = W.arena_bytes;
-    J.tcap = 1u << a.tcap_log2;
-    J.pt = a.pt + (int64_t)blockIdx.x * J.tcap;
-    J.wk = a.wk + (int64_t)blockIdx.x * J.tcap;
-    J.wc = a.wc + (int64_t)blockIdx.x * J.tcap;
-    J.pu = a.used + (int64_t)blockIdx.x * J.tcap;
+    J.tlog2 = W.tlog2;
+    J.tcap = 1u << W.tlog2;
+    J.pt = a.pt + W.tab;
+    J.wk = a.wk + W.tab;
+    J.wc = a.wc + W.tab;
+    J.pu = a.used + W.tab;
     J.wu = J.pu + J.tcap / 2;
     J.var = J.alloc((int64_t)MAXV * n);
     char* A = (char*)J.alloc((int64_t)n * cap);
@@ -863,7 +867,8 @@ __global__ __launch_bounds__(WT) void k_align_wide(WArgs a) {
 
 struct WideBufs {
     DevBuf<wide::WJob> jobs;
-    DevBuf<unsigned char> out[4], arena;
+    std::deque<DevBuf<unsigned char>> outs;  // one output buffer per launch of a call (kept until the next call)
+    DevBuf<unsigned char> arena;
     DevBuf<unsigned long long> pt, wk;
     DevBuf<uint32_t> wc, used;
     DevBuf<int32_t> len, status;
@@ -888,100 +893,143 @@ void align_wide(WideBufs* W, hipStream_t st, const char* d_rows, const int64_t* 
     W->row_len.ensure(n_ne);
     NPGX_HIP(hipMemcpyAsync(W->row_off.p, ne_off, n_ne * 8, hipMemcpyHostToDevice, st));
     NPGX_HIP(hipMemcpyAsync(W->row_len.p, ne_len, n_ne * 4, hipMemcpyHostToDevice, st));
+    // Every job runs until it fits: each attempt gives a failing job more
+    // columns (2x the longest row, 4x, 16x, then the proven bound: the sum of
+    // its rows), larger pair / word tables and a larger arena.  One
+    // try_aligned call inserts at most n x (min tail - aligned_check) pairs
+    // and as many words before its tables are cleared (SimilarAligner.cpp:
+    // 246-308), so tables of 2 (n (longest - ac) + n) entries cannot overflow:
+    // a job's tables stop growing there.  The arena (recursion frames) keeps
+    // doubling.  Jobs of one attempt launch in waves whose scratch fits the
+    // budget (NPGX_WIDE_BUDGET_MB, default 8 GiB); a job that alone needs more
+    // than the budget is refused with NPGX_ERR_RANGE, never cut short.
+    static const int64_t budget = [] {
+        const char* e = getenv("NPGX_WIDE_BUDGET_MB");
+        return (e ? std::max<int64_t>(atoll(e), 64) : 8192) << 20;
+    }();
+    struct Size {
+        int64_t sum, mx;
+        uint32_t lg_need;
+    };
+    std::vector<Size> sz(nj);
+    for (size_t q = 0; q < nj; q++) {
+        const WideJobIn& I = in[q];
+        NPGX_REQUIRE(I.n < 65536, NPGX_ERR_RANGE, "more than 65535 rows in one alignment");
+        int64_t sum = 0, mx = 0;
+        for (int i = 0; i < I.n; i++) {
+            sum += ne_len[I.row0 + i];
+            mx = std::max<int64_t>(mx, ne_len[I.row0 + i]);
+        }
+        NPGX_REQUIRE(sum < (1ll << 30), NPGX_ERR_RANGE, "alignment problem too large");
+        const int64_t need = 2 * ((int64_t)I.n * std::max<int64_t>(mx - params[2], 0) + I.n) + 2;
+        uint32_t lg = 12;
+        while (((int64_t)1 << lg) < need) lg++;
+        sz[q] = Size{sum, mx, lg};
+    }
     std::vector<size_t> todo(nj);
     for (size_t q = 0; q < nj; q++) todo[q] = q;
-    for (int attempt = 0; attempt < 4 && !todo.empty(); attempt++) {
+    size_t launch = 0;
+    for (int attempt = 0; !todo.empty(); attempt++) {
+        NPGX_REQUIRE(attempt < 24, NPGX_ERR_RANGE, "wide alignment: no progress after 24 attempts");
         std::vector<WJob> jobs(todo.size());
-        int64_t out_bytes = 0, arena_bytes = 0;
-        int max_n = 1;
+        std::vector<int64_t> cost(todo.size());
         for (size_t t = 0; t < todo.size(); t++) {
             const WideJobIn& I = in[todo[t]];
-            NPGX_REQUIRE(I.n < 65536, NPGX_ERR_RANGE, "more than 65535 rows in one alignment");
-            int64_t sum = 0, mx = 0;
-            for (int i = 0; i < I.n; i++) {
-                sum += ne_len[I.row0 + i];
-                mx = std::max<int64_t>(mx, ne_len[I.row0 + i]);
-            }
-            NPGX_REQUIRE(sum < (1ll << 30), NPGX_ERR_RANGE, "alignment problem too large");
+            const Size& Z = sz[todo[t]];
             // columns: 2 x the longest row first, then 4x, 16x, the proven bound (the sum)
             const int64_t grow[4] = {2, 4, 16, 1ll << 40};
-            int64_t c = aligner_type == 1 ? mx : std::min<int64_t>(sum, grow[attempt] * mx + 64);
+            int64_t c = aligner_type == 1 ? Z.mx : std::min<int64_t>(Z.sum, grow[std::min(attempt, 3)] * Z.mx + 64);
             c = (std::max<int64_t>(c, 1) + 15) & ~15ll;
             WJob& J = jobs[t];
             J.row0 = I.row0;
             J.n = I.n;
             J.cap = (int32_t)c;
-            J.out = out_bytes;
-            out_bytes += ((int64_t)I.n * c + 255) & ~255ll;
-            J.arena = arena_bytes;
             J.arena_bytes = aligner_type == 1 ? 0
                             : ((4 * (int64_t)I.n * c + 32 * c + (int64_t)I.n * (MAXV + 4 * sizeof(RowV)) + (1 << 16))
-                               << attempt);
-            arena_bytes += (J.arena_bytes + 255) & ~255ll;
-            max_n = std::max(max_n, I.n);
+                               << std::min(attempt, 20));
+            // tables: room for 256 shifts of every row first, x4 per attempt, at most the proven size
+            uint32_t lg = 12;
+            while ((1u << lg) < 512u * (uint32_t)I.n && lg < 22) lg++;
+            J.tlog2 = aligner_type == 1 ? 0 : std::min<uint32_t>(lg + 2 * (uint32_t)attempt, Z.lg_need);
+            const int64_t tab_bytes = aligner_type == 1 ? 0 : ((int64_t)1 << J.tlog2) * 24;
+            cost[t] = (((int64_t)I.n * c + 255) & ~255ll) + ((J.arena_bytes + 255) & ~255ll) + tab_bytes;
+            NPGX_REQUIRE(cost[t] <= budget, NPGX_ERR_RANGE,
+                         "wide alignment problem needs more scratch than NPGX_WIDE_BUDGET_MB allows");
         }
-        // pair/word tables: room for 256 shifts of every row before a re-run
-        uint32_t lg = 12;
-        while ((1u << lg) < 512u * (uint32_t)max_n && lg < 22) lg++;
-        lg = std::min<uint32_t>(lg + 2 * attempt, 24);
-        const size_t tcap = (size_t)1 << lg;
-        W->jobs.ensure(jobs.size());
-        W->out[attempt].ensure(out_bytes);
-        W->arena.ensure(std::max<int64_t>(arena_bytes, 1));
-        const size_t tab = aligner_type == 1 ? 1 : tcap * todo.size();
-        if (W->pt.cap < tab) {
-            W->pt.ensure(tab);
-            W->wk.ensure(tab);
-            NPGX_HIP(hipMemsetAsync(W->pt.p, 0xff, tab * 8, st));
-            NPGX_HIP(hipMemsetAsync(W->wk.p, 0xff, tab * 8, st));
-            W->wc.ensure(tab);
-            NPGX_HIP(hipMemsetAsync(W->wc.p, 0, tab * 4, st));
-            W->used.ensure(tab);
-        }
-        W->len.ensure(jobs.size());
-        W->status.ensure(jobs.size());
-        NPGX_HIP(hipMemcpyAsync(W->jobs.p, jobs.data(), jobs.size() * sizeof(WJob), hipMemcpyHostToDevice, st));
-        WArgs A;
-        A.rows = d_rows;
-        A.row_off = W->row_off.p;
-        A.row_len = W->row_len.p;
-        A.jobs = W->jobs.p;
-        A.out = W->out[attempt].p;
-        A.arena = W->arena.p;
-        A.pt = W->pt.p;
-        A.wk = W->wk.p;
-        A.wc = W->wc.p;
-        A.used = W->used.p;
-        A.tcap_log2 = lg;
-        A.len_out = W->len.p;
-        A.status = W->status.p;
-        A.mc = params[0];
-        A.gc = params[1];
-        A.ac = params[2];
-        A.min_length = params[3];
-        A.wf = params[4];
-        A.aligner_type = aligner_type;
-        hipLaunchKernelGGL(k_align_wide, dim3((unsigned)jobs.size()), dim3(WT), 0, st, A);
-        NPGX_HIP(hipGetLastError());
-        std::vector<int32_t> L(jobs.size()), S(jobs.size());
-        NPGX_HIP(hipMemcpyAsync(L.data(), W->len.p, L.size() * 4, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipMemcpyAsync(S.data(), W->status.p, S.size() * 4, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(stream_wait(st));
         std::vector<size_t> again;
-        for (size_t t = 0; t < todo.size(); t++) {
-            NPGX_REQUIRE(S[t] != 2, NPGX_ERR_RANGE,
-                         "wide alignment: more than 96 nested re-alignments or 8 gap variants");
-            if (S[t] != 0) {
-                again.push_back(todo[t]);
-                continue;
+        for (size_t w0 = 0; w0 < todo.size();) {  // one wave: the jobs [w0, w1)
+            size_t w1 = w0;
+            int64_t used = 0;
+            while (w1 < todo.size() && (w1 == w0 || used + cost[w1] <= budget)) used += cost[w1++];
+            int64_t out_bytes = 0, arena_bytes = 0, tab = 0;
+            for (size_t t = w0; t < w1; t++) {
+                WJob& J = jobs[t];
+                J.out = out_bytes;
+                out_bytes += ((int64_t)J.n * J.cap + 255) & ~255ll;
+                J.arena = arena_bytes;
+                arena_bytes += (J.arena_bytes + 255) & ~255ll;
+                J.tab = tab;
+                tab += aligner_type == 1 ? 0 : (int64_t)1 << J.tlog2;
             }
-            len[todo[t]] = L[t];
-            cap[todo[t]] = jobs[t].cap;
-            ptr[todo[t]] = (const char*)(W->out[attempt].p + jobs[t].out);
+            const size_t nw = w1 - w0;
+            W->jobs.ensure(nw);
+            if (W->outs.size() <= launch) W->outs.emplace_back();
+            DevBuf<unsigned char>& ob = W->outs[launch++];
+            ob.ensure(std::max<int64_t>(out_bytes, 1));
+            W->arena.ensure(std::max<int64_t>(arena_bytes, 1));
+            const size_t tabn = (size_t)std::max<int64_t>(tab, 1);
+            if (W->pt.cap < tabn) {  // a fresh pool is cleared once; the kernel leaves it cleared
+                W->pt.ensure(tabn);
+                W->wk.ensure(tabn);
+                NPGX_HIP(hipMemsetAsync(W->pt.p, 0xff, W->pt.cap * 8, st));
+                NPGX_HIP(hipMemsetAsync(W->wk.p, 0xff, W->wk.cap * 8, st));
+                W->wc.ensure(tabn);
+                NPGX_HIP(hipMemsetAsync(W->wc.p, 0, W->wc.cap * 4, st));
+                W->used.ensure(tabn);
+            }
+            W->len.ensure(nw);
+            W->status.ensure(nw);
+            NPGX_HIP(hipMemcpyAsync(W->jobs.p, jobs.data() + w0, nw * sizeof(WJob), hipMemcpyHostToDevice, st));
+            WArgs A;
+            A.rows = d_rows;
+            A.row_off = W->row_off.p;
+            A.row_len = W->row_len.p;
+            A.jobs = W->jobs.p;
+            A.out = ob.p;
+            A.arena = W->arena.p;
+            A.pt = W->pt.p;
+            A.wk = W->wk.p;
+            A.wc = W->wc.p;
+            A.used = W->used.p;
+            A.len_out = W->len.p;
+            A.status = W->status.p;
+            A.mc = params[0];
+            A.gc = params[1];
+            A.ac = params[2];
+            A.min_length = params[3];
+            A.wf = params[4];
+            A.aligner_type = aligner_type;
+            hipLaunchKernelGGL(k_align_wide, dim3((unsigned)nw), dim3(WT), 0, st, A);
+            NPGX_HIP(hipGetLastError());
+            std::vector<int32_t> L(nw), S(nw);
+            NPGX_HIP(hipMemcpyAsync(L.data(), W->len.p, nw * 4, hipMemcpyDeviceToHost, st));
+            NPGX_HIP(hipMemcpyAsync(S.data(), W->status.p, nw * 4, hipMemcpyDeviceToHost, st));
+            NPGX_HIP(stream_wait(st));
+            for (size_t t = w0; t < w1; t++) {
+                NPGX_REQUIRE(S[t - w0] != 2, NPGX_ERR_RANGE,
+                             "wide alignment: more than 96 nested re-alignments or 8 gap variants");
+                if (S[t - w0] != 0) {
+                    again.push_back(todo[t]);
+                    continue;
+                }
+                len[todo[t]] = L[t - w0];
+                cap[todo[t]] = jobs[t].cap;
+                ptr[todo[t]] = (const char*)(ob.p + jobs[t].out);
+            }
+            w0 = w1;
         }
         todo.swap(again);
     }
-    NPGX_REQUIRE(todo.empty(), NPGX_ERR_RANGE, "wide alignment outgrew its scratch");
 }
 
 }  // namespace npgx

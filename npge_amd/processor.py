@@ -27,6 +27,8 @@ GLOBAL_OPTS = {
     "MISMATCH_CHECK": 1,
     "GAP_CHECK": 2,
     "ALIGNED_CHECK": 10,
+    "MAX_TAIL": 3,           # CMakeLists.txt:89 (MoveGaps)
+    "MAX_TAIL_TO_GAP": "1.0",  # CMakeLists.txt:90 (MoveGaps)
 }
 
 

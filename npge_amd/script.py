@@ -65,7 +65,7 @@ class _EngineProcessor(Processor):
 
 @register
 class MetaAligner(_EngineProcessor):
-    """MetaAligner / Align (MetaAligner.cpp): every unaligned block aligned."""
+    """MetaAligner (MetaAligner.cpp): every unaligned block aligned."""
     name = "MetaAligner"
     engine_name = "MetaAligner"
 
@@ -73,6 +73,57 @@ class MetaAligner(_EngineProcessor):
         super().__init__()
         self.add_gopt("aligner-type", "aligner (the engine's: similar)", "ALIGNER")
         self.add_opt_rule("aligner-type = similar", lambda p: p.opt_value("aligner-type") == "similar")
+
+
+@register
+class Align(MetaAligner):
+    """Align (Align.cpp:36-52): MetaAligner, SelfOverlapsResolver,
+    MetaAligner, then {MoveGaps, CutGaps, Filter} until the block set repeats."""
+    name = "Align"
+    engine_name = "Align"
+
+
+@register
+class LiteAlign(MetaAligner):
+    """LiteAlign (Align.cpp:17-30): MetaAligner, then {MoveGaps, CutGaps}."""
+    name = "LiteAlign"
+    engine_name = "LiteAlign"
+
+
+@register
+class MoveGaps(_EngineProcessor):
+    """MoveGaps (MoveGaps.cpp:21-103): terminal letters moved inside."""
+    name = "MoveGaps"
+
+    def __init__(self):
+        super().__init__()
+        self.add_gopt("max-tail", "Max length of tail", "MAX_TAIL")
+        self.add_gopt("max-tail-to-gap", "Max tail length to gap length ratio", "MAX_TAIL_TO_GAP", Decimal)
+
+    def engine_processor(self):
+        d = self.opt_value("max-tail-to-gap").impl
+        return "MoveGaps --max-tail=%d --max-tail-to-gap=%d.%04d" % (self.opt_value("max-tail"), d // 10000,
+                                                                     d % 10000)
+
+
+@register
+class CutGaps(_EngineProcessor):
+    """CutGaps (CutGaps.cpp:20-159): terminal gap columns cut."""
+    name = "CutGaps"
+
+    def __init__(self):
+        super().__init__()
+        self.add_opt("cut-strict", "cut more gaps", False)
+
+    def engine_processor(self):
+        return "CutGaps --cut-strict=%d" % int(bool(self.opt_value("cut-strict")))
+
+
+@register
+class SelfOverlapsResolver(_EngineProcessor):
+    """SelfOverlapsResolver (SelfOverlapsResolver.cpp:19-22, hit.cpp:68-91)."""
+    name = "SelfOverlapsResolver"
+    engine_name = "SelfOverlapsResolver"
 
 
 @register
@@ -139,11 +190,14 @@ class RemoveAlignment(Processor):
 
 @register
 class Read(Processor):
-    """Read (Read.cpp:36-64) of the program's --in-blocks text."""
+    """Read (Read.cpp:36-64): the program's --in-blocks text when run as the
+    main program (run_main, lua_lib.lua:100-126); no input otherwise."""
     name = "Read"
     in_text = ""
 
     def run_impl(self):
+        if not self.in_text:
+            return
         src = nio.read_blockset(self.in_text)
         bs = self.block_set()
         bs.seqs.extend(src.seqs)
@@ -152,16 +206,23 @@ class Read(Processor):
 
 @register
 class RawWrite(Processor):
-    """RawWrite (RawWrite.cpp:40-59) to the program's --out-file: the script
-    keeps the written set (its text: npge_amd.io.write_blockset)."""
+    """RawWrite (RawWrite.cpp:40-59) to the program's --out-file when run as
+    the main program: the script keeps a snapshot of the set as written (its
+    text: npge_amd.io.write_blockset); later statements do not change it."""
     name = "RawWrite"
+    written = None
 
     def __init__(self):
         super().__init__()
         self.add_opt("skip-rest", "write only blocks", False)
 
     def run_impl(self):
-        pass
+        bs = self.block_set()
+        snap = BlockSet()
+        snap.seqs = list(bs.seqs)
+        snap.blocks = [Block([Fragment(f.seq, f.min_pos, f.max_pos, f.ori, f.row) for f in b.fragments],
+                             name=b.name) for b in bs.blocks]
+        self.written = snap
 
 
 @register
@@ -229,7 +290,7 @@ class Script:
 
     def _proc(self, name, opts, main):
         p = new_p(name)
-        if isinstance(p, Read):
+        if isinstance(p, Read) and main:  # only run_main passes the program arguments
             p.in_text = self.in_text
         if isinstance(opts, dict):
             for k, v in opts.items():
@@ -245,8 +306,8 @@ class Script:
             p.set_bs("other", self.sets["other"])
             p.set_options(opts, self.sets)
         p.run()
-        if isinstance(p, RawWrite):
-            self.out = p.block_set()
+        if isinstance(p, RawWrite) and main:
+            self.out = p.written
         return p
 
     def run(self, text):

@@ -1756,6 +1756,170 @@ static int filter_block(const std::vector<BSeq>& seqs, BBlock& b, const FilterOp
     return 2;
 }
 
+// ---------------------------------------------------------------- MoveGaps / CutGaps
+// The row checks of MoveGaps / CutGaps (MoveGaps.cpp:37-44, CutGaps.cpp:66-74)
+static int64_t checked_rows_length(const BBlock& b) {
+    const int64_t length = block_alignment_length(b);
+    for (const BFrag& f : b.f)
+        if (!f.has_row || (int64_t)f.row.size() != length)
+            throw std::logic_error("No alignment row is set, or its length differs from the block's");
+    return length;
+}
+
+// AlignmentRow::map_to_fragment(col) != -1 on a gapped row (out of range: -1)
+static bool letter_at(const std::string& row, int64_t col) {
+    return col >= 0 && col < (int64_t)row.size() && row[(size_t)col] != '-';
+}
+
+// MoveGaps::move_gaps (MoveGaps.cpp:30-103): a terminal run of at most
+// max_tail letters separated from the rest by a gap run (ending before the
+// middle column) moves inside when tail / gap <= max_tail_to_gap (Decimal:
+// tail * 10^4 / gap, truncated).  Returns whether a row changed.
+static bool move_gaps(BBlock& b, int max_tail, int64_t max_tail_to_gap_x1e4) {
+    const int64_t length = checked_rows_length(b);
+    bool result = false;
+    for (BFrag& f : b.f) {
+        std::pair<int64_t, int64_t> moves[3] = {{0, 0}, {0, 0}, {0, 0}};  // index ori + 1
+        for (int ori = -1; ori <= 1; ori += 2) {
+            const int64_t begin = ori == 1 ? 0 : length - 1;
+            int64_t tail = 0, i;
+            for (i = 0; i < max_tail + 1; i++) {
+                if (letter_at(f.row, begin + i * ori)) tail += 1;
+                else break;
+            }
+            if (0 < tail && tail <= max_tail) {
+                int64_t gap = 0;
+                const int64_t max_pos = length / 2;
+                for (; i < max_pos; i++) {
+                    if (!letter_at(f.row, begin + i * ori)) gap += 1;
+                    else break;
+                }
+                if (i < max_pos && gap != 0 && tail * 10000 / gap <= max_tail_to_gap_x1e4)
+                    moves[ori + 1] = std::make_pair(tail, gap);
+            }
+        }
+        if (moves[0].first != 0 || moves[2].first != 0) {
+            result = true;
+            std::string& data = f.row;
+            for (int ori = -1; ori <= 1; ori += 2) {
+                const int64_t begin = ori == 1 ? 0 : length - 1;
+                const int64_t tail = moves[ori + 1].first, gap = moves[ori + 1].second;
+                if (!tail) continue;
+                for (int64_t i = tail - 1; i >= 0; i--) data[(size_t)(begin + (gap + i) * ori)] = data[(size_t)(begin + i * ori)];
+                for (int64_t i = 0; i < gap; i++) data[(size_t)(begin + i * ori)] = '-';
+            }
+        }
+    }
+    return result;
+}
+
+// CutGaps' slice_fragment (CutGaps.cpp:26-61): the row's columns [from, to];
+// the coordinates move by the letters cut (set_begin_pos / set_last_pos keep
+// the orientation); no letter there -> the fragment leaves the block
+static bool cut_fragment(BFrag& f, int64_t from, int64_t to) {
+    const RowMap m(f.row);
+    int64_t fr_from = -1, fr_to = -1;
+    for (int64_t i = from; i <= to && fr_from == -1; i++) fr_from = m.map_to_fragment(i);
+    if (fr_from == -1) return false;
+    for (int64_t i = to; i >= from && fr_to == -1; i--) fr_to = m.map_to_fragment(i);
+    const int64_t begin = f.begin() + fr_from * f.ori, last = f.begin() + fr_to * f.ori;
+    f.row = f.row.substr((size_t)from, (size_t)(to - from + 1));
+    if (f.ori == 1) {
+        f.min = begin;
+        f.max = last;
+    } else {
+        f.max = begin;
+        f.min = last;
+    }
+    return true;
+}
+
+// CutGaps::cut_gaps (CutGaps.cpp:63-159): strict -- the first and the last
+// gapless column; permissive -- the longest terminal gaps over the rows
+static bool cut_gaps(BBlock& b, bool strict) {
+    const int64_t length = checked_rows_length(b);
+    int64_t from = 0, to = length - 1;
+    if (strict) {
+        auto gapless = [&](int64_t c) {
+            for (const BFrag& f : b.f)
+                if (!letter_at(f.row, c)) return false;
+            return true;
+        };
+        for (; from <= to; from++)
+            if (gapless(from)) break;
+        for (; to >= from; to--)
+            if (gapless(to)) break;
+    } else {
+        for (const BFrag& f : b.f)
+            for (int ori = -1; ori <= 1; ori += 2) {
+                const int64_t begin = ori == 1 ? 0 : length - 1;
+                for (int64_t i = 0; i < length; i++) {
+                    const int64_t al = begin + i * ori;
+                    if (letter_at(f.row, al)) {
+                        if (ori == 1 && al > from) from = al;
+                        else if (ori == -1 && al < to) to = al;
+                        break;
+                    }
+                }
+            }
+    }
+    if (from == 0 && to == length - 1) return false;
+    if (to < from) {
+        b.f.clear();
+        return true;
+    }
+    std::vector<BFrag> kept;
+    for (BFrag& f : b.f)
+        if (cut_fragment(f, from, to)) kept.push_back(std::move(f));
+    b.f.swap(kept);
+    return true;
+}
+
+// ---------------------------------------------------------------- SelfOverlapsResolver
+// has_self_overlaps (hit.cpp:51-66): fragments sorted by (sequence, Fragment
+// operator<) -- Sequence* pinned to the sequence index -- and neighbours
+// tested for common positions
+static bool has_self_overlaps(const BBlock& b) {
+    if (b.f.empty()) return false;
+    std::vector<const BFrag*> v;
+    for (const BFrag& f : b.f) v.push_back(&f);
+    std::sort(v.begin(), v.end(), [](const BFrag* x, const BFrag* y) {
+        if (x->seq != y->seq) return x->seq < y->seq;
+        if (x->min != y->min) return x->min < y->min;
+        if (x->max != y->max) return x->max < y->max;
+        return x->ori < y->ori;
+    });
+    for (size_t i = 0; i + 1 < v.size(); i++)
+        if (v[i]->seq == v[i + 1]->seq && std::max(v[i]->min, v[i + 1]->min) <= std::min(v[i]->max, v[i + 1]->max))
+            return true;
+    return false;
+}
+
+// fix_self_overlaps (hit.cpp:68-91): the block's columns cut back from the
+// end, one at a time, until no two fragments overlap; every fragment is
+// replaced by a row-less one from its begin to the position of that column
+// (fragment_pos, convert_position.cpp:44-67), one-letter ones dropped
+static void fix_self_overlaps(BBlock& b) {
+    if (!has_self_overlaps(b)) return;
+    const BBlock copy = b;
+    const int64_t block_length = block_alignment_length(copy);
+    for (int64_t length = block_length - 1; length >= 0; length--) {
+        b.f.clear();
+        for (const BFrag& f : copy.f) {
+            const int64_t seq_last = f.begin() + f.ori * fragment_pos(f, length, block_length);  // frag_to_seq
+            const int64_t seq_begin = f.begin();
+            if (seq_last != seq_begin) {
+                BFrag nf;
+                nf.seq = f.seq;
+                set_begin_last(nf, seq_begin, seq_last);
+                b.f.push_back(nf);
+            }
+        }
+        if (!has_self_overlaps(b)) break;
+    }
+    if (has_self_overlaps(b)) throw std::logic_error("fix_self_overlaps left an overlap");
+}
+
 // ---------------------------------------------------------------- ExtendLoopFast driver
 struct PipelineOpts {
     SimilarAlignerImpl im;
@@ -1767,7 +1931,51 @@ struct PipelineOpts {
     FilterOpts filter;
     bool do_filter = true;
     int workers = 1;  // BlocksJobs workers (the reference's --workers); 1 = reference-exact sequential run
+    int max_tail = 3;                       // MoveGaps max-tail (MAX_TAIL, CMakeLists.txt:89)
+    int64_t max_tail_to_gap_x1e4 = 10000;   // MoveGaps max-tail-to-gap (MAX_TAIL_TO_GAP 1.0, CMakeLists.txt:90)
 };
+
+// Filter (Filter.cpp:208-248) over every block of the set
+static void filter_all(const std::vector<BSeq>& seqs, std::vector<BBlock>& blocks, const FilterOpts& fo,
+                       int workers) {
+    std::vector<std::vector<BBlock>> subs(blocks.size());
+    std::vector<int> res(blocks.size());
+    for_blocks(blocks.size(), workers, [&](size_t i, int) { res[i] = filter_block(seqs, blocks[i], fo, subs[i]); });
+    std::vector<BBlock> out;
+    for (size_t i = 0; i < blocks.size(); i++) {
+        if (res[i] == 0) out.push_back(std::move(blocks[i]));
+        else if (res[i] == 1)
+            for (auto& x : subs[i]) out.push_back(std::move(x));
+    }
+    blocks.swap(out);
+}
+
+// Align (Align.cpp:36-52): MetaAligner, SelfOverlapsResolver, MetaAligner,
+// then AlignLoop = Pipe{MoveGaps, CutGaps, Filter} with set_max_iterations(-1)
+// (Pipe.cpp:60-78: the block-set hash before the loop and after every lap;
+// a lap ending on a seen hash ends the loop).  lite: LiteAlign (Align.cpp:17-30):
+// MetaAligner, then Pipe{MoveGaps, CutGaps} to the same fixpoint.
+static void align_pipe(BlockSetO& bs, const PipelineOpts& o, bool lite) {
+    const std::vector<BSeq>& seqs = *bs.seqs;
+    auto meta = [&] {
+        for_blocks(bs.blocks.size(), o.workers, [&](size_t i, int) { align_block(seqs, bs.blocks[i], 0, o.im); });
+    };
+    meta();
+    if (!lite) {
+        for (BBlock& b : bs.blocks) fix_self_overlaps(b);
+        meta();
+    }
+    std::set<uint64_t> seen;
+    seen.insert(blockset_hash(bs));
+    while (true) {
+        for (BBlock& b : bs.blocks) move_gaps(b, o.max_tail, o.max_tail_to_gap_x1e4);
+        for (BBlock& b : bs.blocks) cut_gaps(b, false);
+        if (!lite) filter_all(seqs, bs.blocks, o.filter, o.workers);
+        const uint64_t h = blockset_hash(bs);
+        if (seen.count(h)) break;
+        seen.insert(h);
+    }
+}
 
 
 // RemoveNonStem --exact (RemoveNonStem.cpp:29-45)
@@ -1961,19 +2169,7 @@ static void draft_pangenome(std::vector<BSeq>& seqs, AnchorFinder& af, const Pip
     for_blocks(bs.blocks.size(), o.workers,
                [&](size_t i, int) { align_block(seqs, bs.blocks[i], 1, o.im); });  // DummyAligner
     extend_loop_fast(bs, o, st);
-    if (o.do_filter) {
-        std::vector<std::vector<BBlock>> subs(bs.blocks.size());
-        std::vector<int> res(bs.blocks.size());
-        for_blocks(bs.blocks.size(), o.workers,
-                   [&](size_t i, int) { res[i] = filter_block(seqs, bs.blocks[i], o.filter, subs[i]); });
-        std::vector<BBlock> out;
-        for (size_t i = 0; i < bs.blocks.size(); i++) {
-            if (res[i] == 0) out.push_back(std::move(bs.blocks[i]));
-            else if (res[i] == 1)
-                for (auto& x : subs[i]) out.push_back(std::move(x));
-        }
-        bs.blocks.swap(out);
-    }
+    if (o.do_filter) filter_all(seqs, bs.blocks, o.filter, o.workers);
 }
 
 }  // namespace orc
@@ -2200,8 +2396,19 @@ void orc_bs_set_workers(orc_bs* h, int workers) { h->af.workers = h->po.workers 
 // op: 0 FragmentsExtender, 1 FixEnds, 2 Filter, 3 ExtendLoopFast, 4 DummyAligner,
 // 5 RemoveNonStem --exact, 6 DraftPangenome (AnchorFinder on all sequences first),
 // 7 MetaAligner(similar) align_block, 8 Filter::find_good_subblocks, 9 Rest,
-// 10 OverlaplessUnion --ou-move
+// 10 OverlaplessUnion --ou-move, 11 MoveGaps, 12 CutGaps, 13 CutGaps --cut-strict,
+// 14 SelfOverlapsResolver, 15 Align, 16 LiteAlign
+static int bs_apply(orc_bs* h, int op);
+// op codes: see bs_apply; exceptions (the reference's ASSERTs) -> -2
 int orc_bs_apply(orc_bs* h, int op) {
+    try {
+        return bs_apply(h, op);
+    } catch (const std::exception&) {
+        return -2;
+    }
+}
+
+static int bs_apply(orc_bs* h, int op) {
     const std::vector<orc::BSeq>& seqs = h->seqs;
     orc::PipelineOpts& o = h->po;
     std::vector<orc::BBlock> out;
@@ -2255,8 +2462,28 @@ int orc_bs_apply(orc_bs* h, int op) {
             for (auto& b : h->bs.blocks) orc::filter_subblocks(seqs, b, o.filter, out);
             h->bs.blocks.swap(out);
             return 0;
+        case 11:
+            for (auto& b : h->bs.blocks) orc::move_gaps(b, o.max_tail, o.max_tail_to_gap_x1e4);
+            return 0;
+        case 12:
+        case 13:
+            for (auto& b : h->bs.blocks) orc::cut_gaps(b, op == 13);
+            return 0;
+        case 14:
+            for (auto& b : h->bs.blocks) orc::fix_self_overlaps(b);
+            return 0;
+        case 15:
+        case 16:
+            orc::align_pipe(h->bs, o, op == 16);
+            return 0;
     }
     return -1;
+}
+
+// MoveGaps options: max-tail, max-tail-to-gap (x 1e4)
+void orc_bs_set_gap_opts(orc_bs* h, int max_tail, int64_t max_tail_to_gap_x1e4) {
+    h->po.max_tail = max_tail;
+    h->po.max_tail_to_gap_x1e4 = max_tail_to_gap_x1e4;
 }
 
 // [n_blocks, n_fragments, row_bytes, iterations, aligned_residues, anchor_blocks, stem_blocks]

@@ -286,7 +286,8 @@ _PKEYS = list(PIPELINE_DEFAULTS)
 
 OPS = {"FragmentsExtender": 0, "FixEnds": 1, "Filter": 2, "ExtendLoopFast": 3, "DummyAligner": 4,
        "RemoveNonStem": 5, "DraftPangenome": 6, "MetaAligner": 7, "FindGoodSubblocks": 8,
-       "Rest": 9, "OverlaplessUnion": 10}
+       "Rest": 9, "OverlaplessUnion": 10, "MoveGaps": 11, "CutGaps": 12, "CutGapsStrict": 13,
+       "SelfOverlapsResolver": 14, "Align": 15, "LiteAlign": 16}
 
 
 def _bs_lib():
@@ -308,6 +309,7 @@ def _bs_lib():
         L.orc_bs_conseq.restype = i64
         L.orc_bs_deconseq.argtypes = [vp, vp, vp]
         L.orc_bs_deconseq.restype = ctypes.c_int
+        L.orc_bs_set_gap_opts.argtypes = [vp, ctypes.c_int, i64]
         L._bs_bound = True
     return L
 
@@ -315,9 +317,11 @@ def _bs_lib():
 class BlockSetOracle:
     """Oracle block set: sequences + blocks, with the hot-path processors
     (FragmentsExtender, FixEnds, Filter, ExtendLoopFast, DummyAligner,
-    RemoveNonStem, DraftPangenome)."""
+    RemoveNonStem, DraftPangenome, MetaAligner, Rest, OverlaplessUnion,
+    MoveGaps, CutGaps (permissive / strict), SelfOverlapsResolver and the
+    Align / LiteAlign pipes)."""
 
-    def __init__(self, seqs, names, **params):
+    def __init__(self, seqs, names, max_tail=3, max_tail_to_gap_x1e4=10000, **params):
         L = _bs_lib()
         p = dict(PIPELINE_DEFAULTS)
         p.update(params)
@@ -329,6 +333,8 @@ class BlockSetOracle:
         nm = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in names])
         self._h = L.orc_bs_create(n, ctypes.cast(arr, ctypes.c_void_p), _ptr(lens),
                                   ctypes.cast(nm, ctypes.c_void_p), _ptr(prm))
+        # MoveGaps max-tail / max-tail-to-gap (MAX_TAIL 3, MAX_TAIL_TO_GAP 1.0)
+        L.orc_bs_set_gap_opts(self._h, int(max_tail), int(max_tail_to_gap_x1e4))
 
     def __del__(self):
         if getattr(self, "_h", None):

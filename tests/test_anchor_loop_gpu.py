@@ -143,9 +143,10 @@ def test_more_than_64_rows():
 
 
 def test_align_more_than_64_fragments():
-    """MetaAligner (Align) on a block of 80 unaligned repeat copies (mixed
+    """MetaAligner on a block of 80 unaligned repeat copies (mixed
     orientations, widened by random amounts) next to ordinary blocks: rows
-    bit-exact vs the oracle's align_block + refine_alignment."""
+    bit-exact vs the oracle's align_block + refine_alignment; then the whole
+    Align pipe (MoveGaps / CutGaps / Filter on the 80-row block) likewise."""
     import numpy as np
     where = []
     names, seqs = _repeat_genomes(40, where=where)
@@ -153,10 +154,14 @@ def test_align_more_than_64_fragments():
     wide = [(g, max(0, a - int(rng.integers(0, 30))), min(len(seqs[g]) - 1, b + int(rng.integers(0, 30))), o, None)
             for g, a, b, o, _ in where]
     blocks = [wide, wide[:3], wide[10:75]]
-    eng = _engine(seqs, names, blocks).apply("Align")
+    eng = _engine(seqs, names, blocks).apply("MetaAligner")
     o = orc.BlockSetOracle(seqs, names)
     o.set_blocks(blocks)
     o.apply("MetaAligner")
     got = eng.blocks()
     assert got == o.blocks()
     assert max(len(b) for b in got) == 80 and any("-" in (f[4] or "") for b in got for f in b)
+    eng = _engine(seqs, names, blocks).apply("Align")
+    o.set_blocks(blocks)
+    o.apply("Align")
+    assert canon(eng.blocks()) == canon(o.blocks())

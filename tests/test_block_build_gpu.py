@@ -141,7 +141,7 @@ def test_remove_non_stem_fixture(case, opts):
 
 @pytest.mark.parametrize("cfg", ["tiny", "small"])
 def test_meta_aligner(cfg):
-    """MetaAligner / Align (align_block with the similar aligner + refine_alignment)
+    """MetaAligner (align_block with the similar aligner + refine_alignment)
     on unaligned blocks of unequal fragments: the anchors widened by random
     amounts per fragment, single fragments, and already aligned blocks (left
     as they are)."""
@@ -161,7 +161,7 @@ def test_meta_aligner(cfg):
     blocks += b0[420:440]                                   # aligned already
     ss, eng = _engine(seqs, names)
     o = orc.BlockSetOracle(seqs, names)
-    eng.set_blocks(blocks).apply("Align")
+    eng.set_blocks(blocks).apply("MetaAligner")
     o.set_blocks(blocks)
     o.apply("MetaAligner")
     got = eng.blocks()

@@ -149,7 +149,7 @@ def test_draft_pangenome_runs(cfg):
 def test_oracle_workers_identical():
     """The threaded oracle (FragmentTG per sequence in AnchorFinder pass 2,
     BlocksJobs per block, BlocksJobs.cpp:38-240) gives the same blocks as the
-    1-worker run: bench.py's cpu_baseline "all_cores" leg times the same work."""
+    1-worker run: bench.py's cpu_baseline "allotted_cores" leg times the same work."""
     from npge_amd import synth
     names, seqs = synth.genome_set("tiny")
     ref = orc.BlockSetOracle(seqs, names).apply("DraftPangenome")

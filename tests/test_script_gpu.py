@@ -25,6 +25,9 @@ SCRIPTS = {
                      "run_main('Write', '--skip-rest:=1')\n",
     "filter": "run_main('Read')\nrun('Filter', '--find-subblocks=1 --min-identity=1')\nrun_main('RawWrite')\n",
     "stem": "run_main('Read')\nrun('RemoveNonStem', '--exact=0')\nrun_main('RawWrite')\n",
+    # Read; CutGaps permissive / strict; RawWrite
+    "cut_gaps": "run_main('Read')\nrun('CutGaps', '--cut-strict=0')\nrun_main('RawWrite')\n",
+    "cut_gaps_strict": "run_main('Read')\nrun('CutGaps', '--cut-strict=1')\nrun_main('RawWrite')\n",
     "stem-exact": "bs1 = BlockSet.new()\nRead {target=bs1}\nRemoveNonStem {target=bs1, exact=true}\n"
                   "RawWrite {target=bs1}\n",
 }
@@ -42,6 +45,9 @@ def test_script_fixture(script, case):
     exp = nio.read_blockset(open(os.path.join(d, "out.fasta")).read())
     want = blockset_hash(exp.blocks)
     assert output_hash(out) == want
+    if script.startswith("cut_gaps"):  # the rows too
+        assert sorted((f.id(), f.row) for b in out.blocks for f in b.fragments) == \
+            sorted((f.id(), f.row) for b in exp.blocks for f in b.fragments)
     if want == 0:  # (meta_test only warns on an empty expected set: compare the fragments too)
         assert sorted(f.id() for b in out.blocks for f in b.fragments) == \
             sorted(f.id() for b in exp.blocks for f in b.fragments)
@@ -56,6 +62,14 @@ def test_script_grammar_on_cpu():
     out = s.run("-- a comment\nx = BlockSet.new()\nRead {target=x}\nfor i = 1, 2 do\n"
                 "  run('RemoveAlignment', 'target=x') -- '--' inside a comment\nend\n"
                 "run_main('RawWrite', 'target=x --skip-rest:=1')\n")
-    assert out is s.sets["x"] and out.blocks
+    assert out.blocks and out.blocks[0].fragments[0].seq is s.sets["x"].blocks[0].fragments[0].seq
     assert all(f.row is None for b in out.blocks for f in b.fragments)
     assert s.sets["target"].blocks == []
+    # Read / Write see the program arguments only under run_main (lua_lib.lua:100-133);
+    # the written set is a snapshot
+    s2 = Script(text)
+    assert s2.run("run('Read')\nrun('RawWrite')\n") is None
+    assert s2.sets["target"].blocks == []
+    s3 = Script(text)
+    out = s3.run("run_main('Read')\nrun_main('RawWrite')\nrun('RemoveAlignment')\n")
+    assert all(f.row is not None for b in out.blocks for f in b.fragments)

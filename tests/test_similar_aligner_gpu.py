@@ -251,3 +251,40 @@ def test_flank_batch(cfg):
     gpu = BatchAligner().align(jobs)
     bad = [j for j, rows in enumerate(jobs) if orc.align(rows, "align_seqs") != gpu[j]]
     assert not bad, "%d of %d jobs differ (first %d)" % (len(bad), len(jobs), bad[0])
+
+
+def test_refinement_kats_kernel():
+    """src/test/similar_aligner.cpp refinement_3/4/5 through k_refine
+    (npgx_refine_batch)."""
+    from npge_amd.aligner import refine_batch
+    got = refine_batch([["CCGG", "CG-G", "CG-G", "CG-G"], ["CCGGCC", "CGG--C"],
+                        ["-CCCCCC", "CCCACCC", "CCCTCCC"]])
+    assert got == [["CCGG", "C-GG", "C-GG", "C-GG"], ["CCGGCC", "C-GG-C"],
+                   ["CCC-CCC", "CCCACCC", "CCCTCCC"]]
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_refine_random(seed):
+    """k_refine vs the oracle's refine_alignment on the similar aligner's
+    output for random families, and on those alignments with random gaps
+    shuffled in (many moves, pure-gap columns, long gap runs)."""
+    from npge_amd.aligner import refine_batch
+    rng = np.random.default_rng(seed)
+    jobs = [j for j in _random_jobs(seed, 120, nmax=12, lmax=250) if j and any(j)]
+    alns = [orc.align(j, mode="similar") for j in jobs]
+    alns = [a for a in alns if a and a[0]]
+    noisy = []
+    for a in alns:
+        rows = []
+        for r in a:
+            r = list(r)
+            for _ in range(int(rng.integers(0, 6))):
+                p = int(rng.integers(0, len(r)))
+                q = int(rng.integers(0, len(r)))
+                r[p], r[q] = r[q], r[p]  # letters and gaps trade places
+            rows.append("".join(r))
+        noisy.append(rows)
+    for batch in (alns, noisy):
+        got = refine_batch(batch)
+        for a, g in zip(batch, got):
+            assert g == orc.align(a, mode="refine"), a

@@ -6,12 +6,17 @@ resident in HBM: AnchorFinder (k=20, fp=0.1, max 100000 fragments) followed by
 the block build on its anchors (DraftPangenome-equivalent).
 value = input bp of all ranks / max-over-ranks wall time of the K timed steps.
 
-Multi-GPU (torch.distributed.run, one rank per GPU over RCCL), two modes:
-  --mode replicas (default): every rank processes its own genome set (same
-    config, rank-specific seed) -- weak scaling, no data-path collective;
-  --mode sharded: ONE genome set, the AnchorFinder windows and the aligner jobs
-    split over the ranks with RCCL exchanges (npge_amd/comm.py) -- strong
-    scaling; value = that set's bp / time.
+Multi-GPU (torch.distributed.run, one rank per GPU), the same workload at
+every N so that the per-N values compare:
+  --mode sharded (default for N > 1): ONE genome set, the AnchorFinder windows
+    and the aligner jobs split over the ranks, the exchanges on the library's
+    own RCCL communicator over xGMI (npge_amd/comm.py RcclComm) -- strong
+    scaling; value = that set's bp / time;
+  --mode replicas: every rank processes its own genome set (same config,
+    rank-specific seed), no data-path collective -- weak scaling.
+With N > 1 and --mode sharded the line also carries "replicas": the same
+step measured in replica mode right after, for the throughput of N
+independent sets.
 (DESIGN.md "Multi-GPU").
 
 Prints ONE JSON line on rank 0.
@@ -34,7 +39,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3",
                     help="synthetic genome set (npge_amd/synth.py); C3 = the 17-genome ≥50x target config")
-    ap.add_argument("--mode", choices=("replicas", "sharded"), default="replicas")
+    ap.add_argument("--mode", choices=("replicas", "sharded"), default="sharded",
+                    help="N > 1: sharded (one set over the ranks, strong scaling; default) or replicas")
+    ap.add_argument("--no-replicas-line", action="store_true",
+                    help="N > 1 sharded: skip the secondary replica-mode measurement")
     ap.add_argument("--anchor-loop", action="store_true",
                     help="each step also runs one AnchorLoopFast after DraftPangenome (lua_lib.lua:741-758)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -73,8 +81,12 @@ def main():
     ss = _capi.SeqSet(seqs, names)          # resident in HBM before timing
     comm = None
     if sharded:
-        from npge_amd.comm import TorchComm
-        comm = TorchComm(dist, staging="cuda")
+        from npge_amd import comm as ncomm
+        if args.dist_backend == "nccl":
+            comm = ncomm.RcclComm(dist, local_rank)  # the library's own RCCL communicator
+        else:  # gloo rehearsal: ranks may share a GPU (RCCL refuses that)
+            comm = ncomm.TorchComm(dist, staging="cpu")
+        ncomm.check(comm)  # every collective once, results verified, before any timing
     job = pipeline.BlockBuild(ss, names, seqs, comm=comm, anchor_loop=args.anchor_loop)
 
     def step():
@@ -84,6 +96,19 @@ def main():
                                    sync=torch.cuda.synchronize, device="cuda")
     # sharded: the ranks share one set of bp; replicas: each rank has its own
     value = harness.throughput(bp, 1 if sharded else world, args.steps, dt) / 1e6
+    replicas = None
+    if sharded and not args.no_replicas_line:
+        # secondary line: the same step in replica mode (every rank its own set, no collective)
+        rseed = harness.rank_seed(synth.BASE_SEED, rank, args.config)
+        rnames, rseqs = synth.genome_set(args.config, seed=rseed)
+        rss = _capi.SeqSet(rseqs, rnames)
+        rjob = pipeline.BlockBuild(rss, rnames, rseqs, anchor_loop=args.anchor_loop)
+        rdt, _ = harness.timed_steps(rjob.run, args.steps, args.warmup, dist,
+                                     sync=torch.cuda.synchronize, device="cuda")
+        replicas = {"value": round(harness.throughput(synth.total_bp(rseqs), world, args.steps, rdt) / 1e6, 3),
+                    "unit": "Mbp/s", "ms_per_step": round(rdt / args.steps * 1e3, 4), "scaling": "weak",
+                    "parallelism": "replica-per-gpu x%d (independent sets, no collective)" % world}
+        del rjob, rss
 
     # dominant kernel of the last step: algorithmic bytes / HIP-event duration
     # (events recorded on the engine's own stream around each launch)
@@ -147,16 +172,22 @@ def main():
                        "genomes": synth.CONFIGS[args.config][0], "anchor_size": 20,
                        "anchor_fp": 0.1, "max_anchor_fragments": 100000,
                        "inputs": "resident in HBM before the timed region (upload: pcie_inclusive)",
-                       "parallelism": ("sharded x%d (RCCL)" % world) if sharded
+                       "parallelism": ("sharded x%d (one set; %s)" % (world, "library RCCL communicator"
+                                                                       if args.dist_backend == "nccl" else
+                                                                       args.dist_backend)) if sharded
                        else "replica-per-gpu x%d" % world},
             "last_step": info,
             "kernels_last_step": kernels,
             "roofline": roofline,
             "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
+            "replicas": replicas,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        if comm is not None and hasattr(comm, "close"):
+            del job
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -170,6 +170,21 @@ typedef struct {
 
 int npgx_af_run_sharded(npgx_af* af, const npgx_seqset* s, const npgx_comm* comm);
 
+/* A library-owned npgx_comm over RCCL (xGMI), one process per GPU: rank 0
+ * makes the unique id (NPGX_RCCL_ID_BYTES bytes) and the launcher hands it to
+ * every rank before each calls npgx_rccl_comm_create on its own device.  The
+ * collectives run on the communicator's stream with device buffers in and out
+ * (ncclAllReduce, ncclAllGather, grouped ncclBroadcast for the variable
+ * all-gather).  Free with npgx_rccl_comm_free after every handle using it. */
+#define NPGX_RCCL_ID_BYTES 128
+int npgx_rccl_unique_id(void* out);
+int npgx_rccl_comm_create(const void* unique_id, int32_t rank, int32_t world, int32_t device,
+                          npgx_comm** out);
+void npgx_rccl_comm_free(npgx_comm* comm);
+/* Runs every collective of comm on small device buffers and checks the
+ * results (a start-up check of a multi-GPU run; collective on all ranks). */
+int npgx_comm_check(const npgx_comm* comm);
+
 /* Copies bytes between any two of host/device memory (hipMemcpyDefault);
  * for host-side collective adapters. */
 int npgx_memcpy(void* dst, const void* src, int64_t bytes);

@@ -14,7 +14,7 @@ LIB = os.path.join(HERE, "libnpge_amd.so")
 # (loaded by _capi when NPGX_PROFILE=1)
 LIB_PROF = os.path.join(HERE, "libnpge_amd_prof.so")
 SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip", "block_build.hip",
-           "general_aligner.hip", "wide_aligner.hip", "host_sampler.cpp"]
+           "general_aligner.hip", "wide_aligner.hip", "comm_rccl.hip", "host_sampler.cpp"]
 HEADERS = ["common.hpp", "sa_device.hpp", "log_score.inc"]
 ARCH = os.environ.get("NPGX_OFFLOAD_ARCH", "gfx950")
 
@@ -52,7 +52,7 @@ def build(force=False, verbose=False, profile=False):
         if p.returncode != 0:
             raise RuntimeError("hipcc failed on %s:\n%s" % (src, out.decode(errors="replace")))
     tmp = lib + ".tmp"
-    cmd = ["hipcc", "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs
+    cmd = ["hipcc", "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs + ["-lrccl"]
     subprocess.check_call(cmd)
     os.replace(tmp, lib)
     for o in objs:

@@ -1,6 +1,13 @@
-"""Host binding of the library's collectives (``npgx_comm``, include/npge_amd.h)
-to torch.distributed -- the exchange steps of the exactly-sharded AnchorFinder
-(DESIGN.md "Multi-GPU").
+"""The collectives of the exactly-sharded AnchorFinder and block build
+(``npgx_comm``, include/npge_amd.h; SURVEY.md §8e, DESIGN.md "Multi-GPU").
+
+``RcclComm``: the library's own RCCL communicator (npgx_rccl_comm_create) --
+the collectives run natively on its stream over xGMI; Python only hands the
+unique id from rank 0 to the others (one object broadcast at start-up).
+
+``TorchComm``: the same callbacks bound to torch.distributed -- gloo for the
+CPU tests and the one-GPU rehearsal of several ranks (RCCL refuses two ranks
+on one GPU).
 
 One process per GPU.  With the ``nccl`` backend (RCCL over xGMI on MI355X) the
 staging tensors live on the rank's GPU and every exchange is a device-to-device
@@ -118,3 +125,53 @@ class TorchComm:
 
     def pointer(self):
         return ctypes.byref(self.struct)
+
+
+class RcclComm:
+    """npgx_comm owned by the library: RCCL over xGMI, one process per GPU.
+
+    dist: an initialised torch.distributed (any backend) used once, to send
+    rank 0's RCCL unique id to every rank."""
+
+    def __init__(self, dist, device, group=None):
+        from . import _capi
+        L = _capi.lib()
+        if not getattr(L, "_rccl_bound", False):
+            vp = ctypes.c_void_p
+            L.npgx_rccl_unique_id.argtypes = [vp]
+            L.npgx_rccl_comm_create.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                ctypes.POINTER(vp)]
+            L.npgx_rccl_comm_free.argtypes = [vp]
+            L.npgx_rccl_comm_free.restype = None
+            L._rccl_bound = True
+        self._L = L
+        self.errors = []
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        idbuf = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            _capi.check(L.npgx_rccl_unique_id(ctypes.cast(idbuf, ctypes.c_void_p)))
+        obj = [idbuf.raw]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        idbuf = ctypes.create_string_buffer(obj[0], 128)
+        h = ctypes.c_void_p()
+        _capi.check(L.npgx_rccl_comm_create(ctypes.cast(idbuf, ctypes.c_void_p), self.rank, self.world,
+                                            int(device), ctypes.byref(h)))
+        self._h = h
+
+    def pointer(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.npgx_rccl_comm_free(self._h)
+            self._h = None
+
+
+def check(comm):
+    """npgx_comm_check: every collective of `comm` on small device buffers,
+    results verified (collective: call on every rank)."""
+    from . import _capi
+    L = _capi.lib()
+    L.npgx_comm_check.argtypes = [ctypes.c_void_p]
+    _capi.check(L.npgx_comm_check(comm.pointer()))

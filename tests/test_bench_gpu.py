@@ -41,3 +41,5 @@ def test_bench_two_ranks_gloo(mode):
     ranks = 1 if mode == "sharded" else 2
     assert abs(d["value"] - bp * ranks / (d["ms_per_step"] / 1e3) / 1e6) / d["value"] < 1e-3
     assert d["scaling"] == ("strong" if mode == "sharded" else "weak")
+    if mode == "sharded":  # the secondary replica-mode measurement of the same step
+        assert d["replicas"]["value"] > 0 and d["replicas"]["scaling"] == "weak"

@@ -78,7 +78,9 @@ struct AfArgs {
     int32_t k;
     int32_t kb;
     int32_t similar;
-    int32_t pad;
+    int32_t nseg;         // found_collect's output segments (see k_seg_compact)
+    int64_t chunk_base;   // global index of chunks[0] (an epoch's first chunk)
+    int64_t seg_cap;      // entries per output segment
     uint64_t params[MAX_KB];
 };
 
@@ -347,7 +349,31 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
         const int64_t last = min((int64_t)WG, s.size - a.k + 1 - c.pos) - 1;
         if (t == last) blast[0] = f ? 1ull : 0ull;
     }
-    wg_append(col, h, out, n_out);
+    // one of nseg output segments (by global chunk index), each with its own
+    // counter on its own 128-byte line: the workgroups' append atomics spread
+    // over nseg addresses instead of queueing on one (k_seg_compact packs them)
+    const int64_t seg = (a.chunk_base + blockIdx.x) % a.nseg;
+    wg_append(col, h, out + seg * a.seg_cap, n_out + seg * 16);
+}
+
+// the segments of found_collect's output, packed in segment order into out;
+// *total = their sum.  One workgroup per segment (nseg <= 256).
+__global__ __launch_bounds__(256) void k_seg_compact(const uint64_t* __restrict__ hseg,
+                                                     const unsigned long long* __restrict__ ctr, int nseg,
+                                                     int64_t seg_cap, uint64_t* __restrict__ out,
+                                                     unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long part[256];
+    const int j = blockIdx.x, t = threadIdx.x;
+    part[t] = t < j ? ctr[t * 16] : 0ull;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) part[t] += part[t + w];
+        __syncthreads();
+    }
+    const unsigned long long off = part[0];
+    const unsigned long long n = ctr[j * 16];
+    for (unsigned long long i = t; i < n; i += 256) out[off + i] = hseg[(int64_t)j * seg_cap + (int64_t)i];
+    if (j == nseg - 1 && t == 0) *total = off + n;
 }
 
 // this rank's Bloom bit array: the bits its admitted windows set
@@ -488,6 +514,8 @@ struct npgx_af {
     DevBuf<uint32_t> first;
     DevBuf<uint32_t> bloom_bits;  // P of the epoch-filtered pass
     DevBuf<uint64_t> hraw, hsorted, huniq;
+    DevBuf<uint64_t> hseg;                 // found_collect's segmented output (packed into hraw)
+    DevBuf<unsigned long long> segctr;     // its per-segment counters, 16 apart
     DevBuf<unsigned long long> counters;  // [0] = n_raw, [1] = n_unique
     DevBuf<TableSlot> tslots;
     DevBuf<uint32_t> tocc;
@@ -725,6 +753,14 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     af->counters.ensure(8);  // [0] collected, [1] unique, [4..6] sharded boundary
     NPGX_HIP(hipMemsetAsync(af->counters.p, 0, 4 * sizeof(unsigned long long), st));
     af->hraw.ensure((size_t)local_windows + 1);
+    // found_collect appends into nseg segments (global chunk index mod nseg),
+    // each with room for all windows of its chunks
+    A.nseg = (int32_t)std::max<int64_t>(1, std::min<int64_t>(256, nchunks));
+    A.seg_cap = (nchunks + A.nseg - 1) / A.nseg * WG;
+    A.chunk_base = 0;
+    af->hseg.ensure((size_t)(A.nseg * A.seg_cap));
+    af->segctr.ensure((size_t)A.nseg * 16);
+    NPGX_HIP(hipMemsetAsync(af->segctr.p, 0, (size_t)A.nseg * 16 * 8, st));
     size_t ti = 0;
     // bit arrays (uint32 words, W each): P (bits set before this epoch) | Pn
     // (through this one) | this rank's bits | P0 (the lower ranks' bits)
@@ -775,6 +811,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
             const int64_t ne = std::min(per, nchunks - e0);
             AfArgs E = A;
             E.chunks = A.chunks + e0;
+            E.chunk_base = e0;
             const dim3 eg((unsigned)ne);
             ti = af->timer.begin("bloom_first", st, 0.0, 0);
             hipLaunchKernelGGL(k_bloom_first_f, eg, block, 0, st, E, af->first.p, P);
@@ -783,7 +820,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
             ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb) * double(ne) / nchunks, 0);
             const bool more = e0 + ne < nchunks;
             hipLaunchKernelGGL(k_found_collect_f, eg, block, 0, st, E, af->first.p, P, more ? Pn : nullptr,
-                               af->hraw.p, af->counters.p, P0, e0 == 0 ? bfirst : nullptr,
+                               af->hseg.p, af->segctr.p, P0, e0 == 0 ? bfirst : nullptr,
                                more ? nullptr : blast);
             NPGX_HIP(hipGetLastError());
             af->timer.end(ti, st);
@@ -795,8 +832,15 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         NPGX_HIP(hipGetLastError());
         af->timer.end(ti, st);
         ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb), local_windows);
-        hipLaunchKernelGGL(k_found_collect_f, grid, block, 0, st, A, af->first.p, P, nullptr, af->hraw.p,
-                           af->counters.p, P0, bfirst, blast);
+        hipLaunchKernelGGL(k_found_collect_f, grid, block, 0, st, A, af->first.p, P, nullptr, af->hseg.p,
+                           af->segctr.p, P0, bfirst, blast);
+        NPGX_HIP(hipGetLastError());
+        af->timer.end(ti, st);
+    }
+    if (run_local) {  // the collected hashes packed into hraw, their count into counters[0]
+        ti = af->timer.begin("collect_pack", st, 0.0, 0);
+        hipLaunchKernelGGL(k_seg_compact, dim3((unsigned)A.nseg), dim3(256), 0, st, af->hseg.p, af->segctr.p,
+                           A.nseg, A.seg_cap, af->hraw.p, af->counters.p);
         NPGX_HIP(hipGetLastError());
         af->timer.end(ti, st);
     }

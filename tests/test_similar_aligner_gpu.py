@@ -288,3 +288,21 @@ def test_refine_random(seed):
         got = refine_batch(batch)
         for a, g in zip(batch, got):
             assert g == orc.align(a, mode="refine"), a
+
+
+def test_wide_unrelated_long_tails():
+    """More than 64 rows whose homology ends after a short core, followed by
+    unrelated tails of 20k+ bases: the wide aligner's word
+    search scans ~20k shifts x 70 rows before giving up; its tables grow to
+    the proven size on a retry instead of failing, and the rows match the
+    oracle."""
+    rng = np.random.default_rng(99)
+    core = rng.integers(0, 4, 200)
+    rows = []
+    for _ in range(70):
+        c = core.copy()
+        m = rng.random(len(c)) < 0.01
+        c[m] = (c[m] + 1) % 4
+        tail = rng.integers(0, 4, int(rng.integers(20000, 21000)))
+        rows.append("".join("ATGC"[x] for x in np.concatenate([c, tail])))
+    _check([rows])

@@ -81,6 +81,8 @@ struct AfArgs {
     int32_t nseg;         // found_collect's output segments (see k_seg_compact)
     int64_t chunk_base;   // global index of chunks[0] (an epoch's first chunk)
     int64_t seg_cap;      // entries per output segment
+    uint8_t* wmask;       // per window (chunk index * WG + thread): k_bloom_first_f's P test for
+                          // k_found_collect_f (bit 7 admitted, bit i: bit i in P); null: not used
     uint64_t params[MAX_KB];
 };
 
@@ -218,13 +220,21 @@ __device__ __forceinline__ bool bit_in(const uint32_t* __restrict__ P, uint32_t 
     return (P[idx >> 5] >> (idx & 31)) & 1u;
 }
 
+// With a.wmask (kb <= FKB) the P test of every window is kept for
+// k_found_collect_f of the same epoch (P does not change in between): one
+// coalesced byte per window instead of kb random P loads there again (P is
+// m/8 bytes: 45 MB at C5, past the L2s, where random loads run at about 55 G/s).
 __global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __restrict__ first,
                                                       const uint32_t* __restrict__ P) {
     const Chunk c = a.chunks[blockIdx.x];
     const SeqMeta s = a.meta[c.seq];
     const int64_t p = c.pos + threadIdx.x;
     uint64_t h, dir;
-    if (!admitted(a, s, p, h, dir)) return;
+    uint8_t* wm = a.wmask ? a.wmask + (a.chunk_base + blockIdx.x) * WG + threadIdx.x : nullptr;
+    if (!admitted(a, s, p, h, dir)) {
+        if (wm) *wm = 0;
+        return;
+    }
     const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
     if (a.kb <= FKB) {
         uint32_t idx[FKB], pw[FKB];
@@ -234,9 +244,15 @@ __global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __rest
                 idx[i] = bloom_index(h ^ a.params[i], a.m, a.mmagic);
                 pw[i] = P[idx[i] >> 5];
             }
+        uint32_t v = 0x80u;
 #pragma unroll
         for (int i = 0; i < FKB; i++)
-            if (i < a.kb && !((pw[i] >> (idx[i] & 31)) & 1u)) atomicMin(&first[idx[i]], ord);
+            if (i < a.kb) {
+                const uint32_t in = (pw[i] >> (idx[i] & 31)) & 1u;
+                v |= in << i;
+                if (!in) atomicMin(&first[idx[i]], ord);
+            }
+        if (wm) *wm = (uint8_t)v;
         return;
     }
     for (int i = 0; i < a.kb; i++) {
@@ -283,7 +299,34 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
     const int64_t p = c.pos + t;
     uint64_t h = 0;
     bool f = false;
-    {
+    if (a.wmask) {
+        // k_bloom_first_f's admission and P test (kb <= FKB): the first[]
+        // entries of the bits outside P are the only random loads left
+        const uint32_t v = a.wmask[(a.chunk_base + blockIdx.x) * WG + t];
+        if (v & 0x80u) {
+            const int64_t w = s.word_off + (p >> 5);
+            const int sh = (int)(p & 31) * 2;
+            const uint64_t lo = a.words[w], hi = a.words[w + 1];
+            const uint64_t dir = (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo) & a.kmask;
+            const uint64_t rev = revcomp(dir, a.k);
+            h = dir < rev ? dir : rev;
+            const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
+            f = true;
+            uint32_t idx[FKB], fv[FKB];
+#pragma unroll
+            for (int i = 0; i < FKB; i++)
+                if (i < a.kb && !((v >> i) & 1u)) {
+                    idx[i] = bloom_index(h ^ a.params[i], a.m, a.mmagic);
+                    fv[i] = first[idx[i]];
+                }
+#pragma unroll
+            for (int i = 0; i < FKB; i++)
+                if (i < a.kb && !((v >> i) & 1u)) {
+                    f &= fv[i] < ord;
+                    if (Pn && fv[i] == ord) atomicOr(&Pn[idx[i] >> 5], 1u << (idx[i] & 31));
+                }
+        }
+    } else {
         uint64_t dir;
         if (admitted(a, s, p, h, dir)) {
             const uint32_t ord = (uint32_t)(s.order_off + (uint64_t)p);
@@ -375,6 +418,48 @@ __global__ __launch_bounds__(256) void k_seg_compact(const uint64_t* __restrict_
     for (unsigned long long i = t; i < n; i += 256) out[off + i] = hseg[(int64_t)j * seg_cap + (int64_t)i];
     if (j == nseg - 1 && t == 0) *total = off + n;
 }
+
+// Up to 8 buffers set to a 32-bit pattern in ONE launch (the run's resets:
+// first[], the bit arrays, the counters; the table's slots and counts), instead
+// of one fill dispatch each.  blockIdx.y = buffer; 16-byte stores where the
+// buffer is 16-byte aligned and a multiple of 4 words.
+struct FillOp {
+    uint32_t* p;
+    int64_t n;  // 32-bit words
+    uint32_t v;
+};
+struct FillArgs {
+    FillOp op[8];
+};
+__global__ __launch_bounds__(256) void k_fill_multi(FillArgs f) {
+    const FillOp o = f.op[blockIdx.y];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (((uintptr_t)o.p & 15) == 0 && (o.n & 3) == 0) {
+        uint4* q = (uint4*)o.p;
+        const uint4 v = make_uint4(o.v, o.v, o.v, o.v);
+        for (int64_t i = t; i < o.n / 4; i += stride) q[i] = v;
+    } else {
+        for (int64_t i = t; i < o.n; i += stride) o.p[i] = o.v;
+    }
+}
+
+struct Fills {
+    FillArgs a{};
+    int n = 0;
+    void add(void* p, int64_t bytes, uint32_t v) {
+        if (bytes <= 0) return;
+        a.op[n++] = FillOp{(uint32_t*)p, bytes / 4, v};
+    }
+    void launch(hipStream_t st) {
+        if (n == 0) return;
+        int64_t most = 0;
+        for (int i = 0; i < n; i++) most = std::max(most, a.op[i].n);
+        const unsigned gx = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (most / 4 + 255) / 256));
+        hipLaunchKernelGGL(k_fill_multi, dim3(gx, (unsigned)n), dim3(256), 0, st, a);
+        n = 0;
+    }
+};
 
 // this rank's Bloom bit array: the bits its admitted windows set
 __global__ __launch_bounds__(WG) void k_bloom_bits(AfArgs a, uint32_t* __restrict__ bits) {
@@ -516,6 +601,7 @@ struct npgx_af {
     DevBuf<uint64_t> hraw, hsorted, huniq;
     DevBuf<uint64_t> hseg;                 // found_collect's segmented output (packed into hraw)
     DevBuf<unsigned long long> segctr;     // its per-segment counters, 16 apart
+    DevBuf<uint8_t> wmask;                 // per window: bloom_first's P test for found_collect
     DevBuf<unsigned long long> counters;  // [0] = n_raw, [1] = n_unique
     DevBuf<TableSlot> tslots;
     DevBuf<uint32_t> tocc;
@@ -751,7 +837,8 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     // --- pass 1: Bloom first-setter + found/collect
     af->first.ensure((size_t)m);
     af->counters.ensure(8);  // [0] collected, [1] unique, [4..6] sharded boundary
-    NPGX_HIP(hipMemsetAsync(af->counters.p, 0, 4 * sizeof(unsigned long long), st));
+    Fills fills;  // the run's resets, one launch (k_fill_multi)
+    fills.add(af->counters.p, 4 * sizeof(unsigned long long), 0u);
     af->hraw.ensure((size_t)local_windows + 1);
     // found_collect appends into nseg segments (global chunk index mod nseg),
     // each with room for all windows of its chunks
@@ -760,7 +847,11 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     A.chunk_base = 0;
     af->hseg.ensure((size_t)(A.nseg * A.seg_cap));
     af->segctr.ensure((size_t)A.nseg * 16);
-    NPGX_HIP(hipMemsetAsync(af->segctr.p, 0, (size_t)A.nseg * 16 * 8, st));
+    fills.add(af->segctr.p, (int64_t)A.nseg * 16 * 8, 0u);
+    if (kb <= FKB && nchunks > 0) {  // every byte is written by k_bloom_first_f before it is read
+        af->wmask.ensure((size_t)nchunks * WG);
+        A.wmask = af->wmask.p;
+    }
     size_t ti = 0;
     // bit arrays (uint32 words, W each): P (bits set before this epoch) | Pn
     // (through this one) | this rank's bits | P0 (the lower ranks' bits)
@@ -773,8 +864,15 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     unsigned long long* bfirst = comm ? af->counters.p + 4 : nullptr;
     unsigned long long* blast = comm ? af->counters.p + 6 : nullptr;
     ti = af->timer.begin("bloom_first", st, local_windows * (0.375 + 8.0 * kb), local_windows);
-    NPGX_HIP(hipMemsetAsync(af->first.p, 0xFF, (size_t)m * 4, st));
-    if (comm) NPGX_HIP(hipMemsetAsync(af->counters.p + 4, 0, 3 * 8, st));
+    fills.add(af->first.p, m * 4, 0xFFFFFFFFu);
+    if (comm) {
+        fills.add(af->counters.p + 4, 3 * 8, 0u);
+        fills.add(mine, W * 4, 0u);
+    } else {
+        fills.add(P, 2 * W * 4, 0u);
+    }
+    fills.launch(st);
+    NPGX_HIP(hipGetLastError());
     af->timer.end(ti, st);
     if (comm) {
         // exchange 1: every rank's Bloom bit array (m / 8 bytes); this rank
@@ -784,7 +882,6 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         // P0) -- the reference's sequential test exactly.  P and Pn start at P0.
         P0 = P + 3 * W;
         ti = af->timer.begin("bloom_bits_exchange", st, (double)m / 8 * world, m);
-        NPGX_HIP(hipMemsetAsync(mine, 0, (size_t)W * 4, st));
         if (run_local) hipLaunchKernelGGL(k_bloom_bits, grid, block, 0, st, A, mine);
         NPGX_HIP(hipGetLastError());
         std::vector<int64_t> cnt(world, w64);
@@ -798,15 +895,17 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         NPGX_HIP(hipMemcpyAsync(P, P0, (size_t)W * 4, hipMemcpyDeviceToDevice, st));
         NPGX_HIP(hipMemcpyAsync(Pn, P0, (size_t)W * 4, hipMemcpyDeviceToDevice, st));
         af->timer.end(ti, st);
-    } else {
-        NPGX_HIP(hipMemsetAsync(P, 0, (size_t)(2 * W) * 4, st));
     }
     if (af->opt.bloom_epochs != 1 && run_local) {
         // epochs of consecutive chunks (SeqMeta order); bits set by earlier
-        // epochs (or lower ranks) skip the atomics and the first[] reads
-        const int64_t per = std::max<int64_t>(1, (int64_t)std::ceil(double(nchunks) / std::max(1, af->opt.bloom_epochs > 0
-                                                                         ? af->opt.bloom_epochs
-                                                                         : (int)std::max<int64_t>(1, local_windows / (2 << 20)))));
+        // epochs (or lower ranks) skip the atomics and the first[] reads.
+        // Automatic count: one epoch per 2 M windows, at most 24 (each epoch
+        // costs two launches and a copy of the m/8-byte bit array; past ~20
+        // epochs the filtering gains nothing more: C5 sweep)
+        const int auto_epochs = (int)std::min<int64_t>(24, std::max<int64_t>(1, local_windows / (2 << 20)));
+        const int64_t per = std::max<int64_t>(
+            1, (int64_t)std::ceil(double(nchunks) / std::max(1, af->opt.bloom_epochs > 0 ? af->opt.bloom_epochs
+                                                                                          : auto_epochs)));
         for (int64_t e0 = 0; e0 < nchunks; e0 += per) {
             const int64_t ne = std::min(per, nchunks - e0);
             AfArgs E = A;
@@ -940,8 +1039,15 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         af->tocc.ensure((size_t)(cap + 31) / 32);
         TableArgs T{af->tslots.p, af->tocc.p, (uint32_t)(cap - 1), 64 - log2cap};
         ti = af->timer.begin("table_insert", st, nH * 8.0 + nH * 12.0, nH);
-        NPGX_HIP(hipMemsetAsync(af->tslots.p, 0xFF, cap * sizeof(TableSlot), st));
-        NPGX_HIP(hipMemsetAsync(af->tocc.p, 0, (size_t)(cap + 31) / 32 * 4, st));
+        af->counts.ensure((size_t)nH);
+        af->offsets.ensure((size_t)nH);
+        af->cursor.ensure((size_t)nH);
+        fills.add(af->tslots.p, (int64_t)(cap * sizeof(TableSlot)), 0xFFFFFFFFu);
+        fills.add(af->tocc.p, (int64_t)(cap + 31) / 32 * 4, 0u);
+        fills.add(af->counts.p, nH * 4, 0u);
+        fills.add(af->cursor.p, nH * 4, 0u);
+        fills.launch(st);
+        NPGX_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_table_insert, dim3((unsigned)((nH + 255) / 256)), dim3(256), 0, st,
                            af->huniq.p, nH, af->tslots.p, af->tocc.p, (uint32_t)(cap - 1),
                            64 - log2cap);
@@ -949,11 +1055,6 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         af->timer.end(ti, st);
 
         // --- pass 2a: FoundFragment counts per hash
-        af->counts.ensure((size_t)nH);
-        af->offsets.ensure((size_t)nH);
-        af->cursor.ensure((size_t)nH);
-        NPGX_HIP(hipMemsetAsync(af->counts.p, 0, (size_t)nH * 4, st));
-        NPGX_HIP(hipMemsetAsync(af->cursor.p, 0, (size_t)nH * 4, st));
         ti = af->timer.begin("ff_count", st, local_windows * (0.375 + 12.0), local_windows);
         if (run_local) hipLaunchKernelGGL(k_ff_count, grid, block, 0, st, A, T, af->counts.p);
         NPGX_HIP(hipGetLastError());

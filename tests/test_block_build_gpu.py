@@ -178,19 +178,27 @@ def _ou_blocks(rng, n_seqs, seq_len, n_blocks, max_len, self_overlap=False):
             mn = int(rng.integers(0, seq_len - max_len))
             frs.append((int(s), mn, mn + int(rng.integers(0, max_len)), int(rng.choice([-1, 1])), None))
         blocks.append(frs)
-    if self_overlap:  # a block overlapping itself: the ordered multiset mode
+    if self_overlap is True:  # a block overlapping itself: the ordered multiset mode
         s, mn, mx, ori, _ = blocks[7][0]
         blocks[7].append((s, mn, mx + 5, -ori, None))
+    elif self_overlap:  # that many, spread over the order, some reaching far (free ones included)
+        for i in rng.choice(n_blocks, size=self_overlap, replace=False):
+            s, mn, mx, ori, _ = blocks[i][0]
+            ext = int(rng.integers(0, 2000)) if i % 3 == 0 else int(rng.integers(0, 10))
+            a = max(0, mn - int(rng.integers(0, 5)))
+            blocks[i].append((s, a, min(seq_len - 1, mx + ext), -ori, None))
     return blocks
 
 
-@pytest.mark.parametrize("max_len,self_overlap", [(40, False), (400, False), (3000, False), (40, True)])
+@pytest.mark.parametrize("max_len,self_overlap", [(40, False), (400, False), (3000, False), (40, True),
+                                                  (40, 60), (400, 60), (3000, 60)])
 def test_overlapless_union_many_blocks(max_len, self_overlap):
-    """OverlaplessUnion --ou-move over 1500 blocks: sparse (the threaded
-    conflict pre-pass admits most blocks directly), dense (most rejected),
-    long fragments past the interval-map threshold, and a self-overlapping
-    block (pre-pass declines); then a second call on the same engine, which
-    after a high rejection rate takes the ordered test for every block."""
+    """OverlaplessUnion --ou-move over 1500 blocks: sparse (most blocks in
+    conflict with no other: admitted by free_blocks without the sequential
+    test), dense (most rejected), long fragments past the interval-map
+    threshold, one or 60 self-overlapping blocks (the ordered multiset mode,
+    switched on by free and by conflicting blocks); then a second call on the
+    same engine (only the touched bitmap ranges cleared in between)."""
     import numpy as np
     rng = np.random.default_rng(max_len + self_overlap)
     n_seqs, seq_len = 8, 400000

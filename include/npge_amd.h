@@ -424,6 +424,13 @@ int npgx_dp_kernel_times(const npgx_dp* dp, npgx_kernel_time* out, int32_t cap, 
 int npgx_dp_phase_cycles(const npgx_dp* dp, int64_t* fwd, int64_t* back, int64_t* steps);
 void npgx_dp_free(npgx_dp* dp);
 
+/* ---- diagnostics (host only, no device needed) ---- */
+/* goodSlices (goodSlices.cpp:247-255) over n column scores as Filter runs it
+ * (replaces GoodSlicer::calculate): the slices' (start, stop) pairs into out
+ * (at most max_out pairs); returns their count, -1 on bad arguments. */
+int npgx_diag_good_slices(const int32_t* scores, int32_t n, int32_t frame_length, int32_t end_length,
+                          int32_t min_identity, int32_t min_length, int64_t* out, int32_t max_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1676,29 +1676,47 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
 // The rows of the bad regions k_split_post queued (SaSub.pad = the region's
 // width): columns [x, x + width) of every row of the job's A, gap-filtered
 // and reversed into C at column x (fix_bad_regions :443-447), the lengths
-// into the sub-job's pool header; one wave per (sub-job, row)
+// into the sub-job's pool header; one wave per sub-job, its rows in turn (a
+// wave per (sub-job, row slot) read the sub-job and job records 64 times per
+// sub-job, most of them for rows the job does not have: 11 ms at C5)
 __global__ __launch_bounds__(256) void k_sub_rows(SaArgs a) {
-    const unsigned long long n_pairs = a.alloc[1] * 64ull;
+    const unsigned long long n_sub = a.alloc[1];
     const int lane = threadIdx.x & 63;
-    for (unsigned long long p = blockIdx.x * 4ull + (threadIdx.x >> 6); p < n_pairs; p += gridDim.x * 4ull) {
-        const SaSub d = a.subs[p >> 6];
-        const int r = (int)(p & 63);
+    for (unsigned long long q = blockIdx.x * 4ull + (threadIdx.x >> 6); q < n_sub; q += gridDim.x * 4ull) {
+        const SaSub d = a.subs[q];
         if (d.pad <= 0) continue;
         const SaJob job = a.jobs[d.job];
-        if (r >= job.n) continue;
-        const char* src = (const char*)(a.scratch + job.scratch) + (size_t)r * job.cap;
-        char* dst = (char*)(a.scratch + job.scratch) + (2 * (size_t)job.n + r) * job.cap + d.x;
-        int k = 0;
-        for (int base = d.x + d.pad - 1; base >= d.x; base -= 64) {
-            const int idx = base - lane;
-            const bool in = idx >= d.x;
-            const char x = in ? src[idx] : '-';
-            const bool keep = in && x != '-';
-            const unsigned long long m = ballot(keep);
-            if (keep) dst[k + __popcll(m & ((1ull << lane) - 1ull))] = x;
-            k += __popcll(m);
+        for (int r = 0; r < job.n; r++) {
+            const char* src = (const char*)(a.scratch + job.scratch) + (size_t)r * job.cap;
+            char* dst = (char*)(a.scratch + job.scratch) + (2 * (size_t)job.n + r) * job.cap + d.x;
+            int k = 0;
+            // 1024 columns per step (16 a lane, from the top down): the lane's
+            // letters counted, a wave prefix sum places them (long bad regions --
+            // tens of thousands of columns at C5 -- took one step per 64 columns)
+            for (int top = d.x + d.pad - 1; top >= d.x; top -= 1024) {
+                const int hi = top - 16 * lane;  // this lane's columns hi, hi-1, .., hi-15
+                char x[16];
+                int cnt = 0;
+    #pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int idx = hi - u;
+                    x[u] = idx >= d.x ? src[idx] : '-';
+                    cnt += x[u] != '-';
+                }
+                int pre = cnt;  // inclusive prefix over the lanes
+    #pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(pre, o);
+                    if (lane >= o) pre += t;
+                }
+                int at = k + pre - cnt;
+    #pragma unroll
+                for (int u = 0; u < 16; u++)
+                    if (x[u] != '-') dst[at++] = x[u];
+                k += __shfl(pre, 63);
+            }
+            if (lane == 0) ((int*)(a.pool + d.out_off))[r] = k;
         }
-        if (lane == 0) ((int*)(a.pool + d.out_off))[r] = k;
     }
 }
 

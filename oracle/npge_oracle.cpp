@@ -2525,6 +2525,19 @@ void orc_bs_copy(const orc_bs* h, int64_t* block_start, int32_t* seq, int64_t* m
 
 uint64_t orc_bs_hash(const orc_bs* h) { return orc::blockset_hash(h->bs); }
 
+// goodSlices (goodSlices.cpp:247-255) over n column scores: the slices'
+// (start, stop) pairs into out (at most max_out); returns their count
+int orc_good_slices(const int32_t* scores, int n, int frame_length, int end_length, int min_identity, int min_length,
+                    int64_t* out, int max_out) {
+    const std::vector<int> sc(scores, scores + n);
+    const std::vector<orc::SS> r = orc::GoodSlicer(sc, frame_length, end_length, min_identity, min_length).calculate();
+    for (size_t i = 0; i < r.size() && (int)i < max_out; i++) {
+        out[2 * i] = r[i].first;
+        out[2 * i + 1] = r[i].second;
+    }
+    return (int)r.size();
+}
+
 // goodColumns (goodColumns.cpp:177-209) of nrows rows of `length` chars each
 int orc_good_columns(int nrows, const char* rows, int length, int min_identity, int min_length, int32_t* out) {
     Strings r((size_t)nrows);

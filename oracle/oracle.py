@@ -102,6 +102,9 @@ def lib():
                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int, P32, P32, P32, vp, P32]
         L.orc_ga_align.restype = ctypes.c_int
+        L.orc_good_slices.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      vp, ctypes.c_int]
+        L.orc_good_slices.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -140,6 +143,16 @@ def optimal_bits(members, p):
 
 def optimal_hashes(members, bits):
     return lib().orc_optimal_hashes(members, bits)
+
+
+def good_slices(scores, frame_length, end_length, min_identity, min_length):
+    """goodSlices (goodSlices.cpp:247-255) over column scores: [(start, stop)]."""
+    L = lib()
+    sc = np.ascontiguousarray(scores, dtype=np.int32)
+    cap = len(sc) + 1
+    out = np.zeros(2 * cap, dtype=np.int64)
+    n = L.orc_good_slices(_ptr(sc), len(sc), frame_length, end_length, min_identity, min_length, _ptr(out), cap)
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
 
 
 def weight_factor(min_identity_x1e4):

@@ -1676,17 +1676,18 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
 // The rows of the bad regions k_split_post queued (SaSub.pad = the region's
 // width): columns [x, x + width) of every row of the job's A, gap-filtered
 // and reversed into C at column x (fix_bad_regions :443-447), the lengths
-// into the sub-job's pool header; one wave per sub-job, its rows in turn (a
-// wave per (sub-job, row slot) read the sub-job and job records 64 times per
-// sub-job, most of them for rows the job does not have: 11 ms at C5)
-__global__ __launch_bounds__(256) void k_sub_rows(SaArgs a) {
-    const unsigned long long n_sub = a.alloc[1];
+// into the sub-job's pool header; one wave per (sub-job, row) for the rows
+// the batch's jobs have (`rows`, not 64 row slots: each slot reread the
+// sub-job and job records -- 11 ms at C5's 8-row jobs)
+__global__ __launch_bounds__(256) void k_sub_rows(SaArgs a, int rows) {
+    const unsigned long long n_pairs = a.alloc[1] * (unsigned long long)rows;
     const int lane = threadIdx.x & 63;
-    for (unsigned long long q = blockIdx.x * 4ull + (threadIdx.x >> 6); q < n_sub; q += gridDim.x * 4ull) {
-        const SaSub d = a.subs[q];
+    for (unsigned long long p = blockIdx.x * 4ull + (threadIdx.x >> 6); p < n_pairs; p += gridDim.x * 4ull) {
+        const SaSub d = a.subs[p / rows];
         if (d.pad <= 0) continue;
         const SaJob job = a.jobs[d.job];
-        for (int r = 0; r < job.n; r++) {
+        const int r = (int)(p % rows);
+        if (r < job.n) {
             const char* src = (const char*)(a.scratch + job.scratch) + (size_t)r * job.cap;
             char* dst = (char*)(a.scratch + job.scratch) + (2 * (size_t)job.n + r) * job.cap + d.x;
             int k = 0;
@@ -2945,7 +2946,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             al->d_reg_dst.grow((size_t)n_reg + jobs.size());
             if (!splits.empty()) {  // the rows of the split jobs' bad regions
                 ti = al->timer.begin("align_sub_rows", st, 0.0, 0);
-                hipLaunchKernelGGL(k_sub_rows, dim3(1024), dim3(256), 0, st, A);
+                hipLaunchKernelGGL(k_sub_rows, dim3(1024), dim3(256), 0, st, A, max_n);
                 NPGX_HIP(hipGetLastError());
                 al->timer.end(ti, st);
             }

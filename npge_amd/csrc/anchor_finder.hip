@@ -1031,7 +1031,12 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     if (nH > 0) {
         // --- membership table
         uint64_t cap = 1024;
-        while (cap < 2ull * (uint64_t)nH) cap <<= 1;
+        // at least 4 slots per hash (NPGX_AF_TABLE_SLOTS overrides): a
+        // non-member window reads a slot line only when its home slot is
+        // taken -- C3 ff_count 0.82 -> 0.63 ms from 2 to 4 slots, C5
+        // 6.9 -> 6.1 ms (`profiles/r03y_table_slots.txt`)
+        static const uint64_t spf = getenv("NPGX_AF_TABLE_SLOTS") ? std::max(2, atoi(getenv("NPGX_AF_TABLE_SLOTS"))) : 4;
+        while (cap < spf * (uint64_t)nH) cap <<= 1;
         NPGX_REQUIRE(cap <= (1ull << 31), NPGX_ERR_RANGE, "hash set too large");
         int log2cap = 0;
         while ((1ull << log2cap) < cap) log2cap++;

@@ -27,6 +27,10 @@
 #include "common.hpp"
 #include "sa_device.hpp"
 
+#ifndef SA_WAVES_PER_EU
+#define SA_WAVES_PER_EU 4
+#endif
+
 namespace npgx {
 
 using namespace sa;
@@ -882,7 +886,7 @@ __device__ __forceinline__ int fin_width(const SaArgs& a, int4 rg) {
 // k_align_sub: every bad region of every deferred job, one wave each; with a
 // plan (k_plan_subs) the segments of the split sub-jobs first, then the other
 // sub-jobs
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_sub(SaArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER_EU))) void k_align_sub(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
     SlotEnv e = slot_env(a, lds_u64);
@@ -1927,9 +1931,6 @@ __global__ __launch_bounds__(POST_THREADS) void k_fin_copy(SaArgs a, int lds_int
     }
 }
 
-#ifndef SA_WAVES_PER_EU
-#define SA_WAVES_PER_EU 4
-#endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER_EU))) void k_align_jobs(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
@@ -2015,21 +2016,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
                 C = B + (size_t)n * cap;
             }
             if (tot <= sb) {
-                for (int r = 0; r < n; r++) {
-                    const char* src = bcast_ptr(v0.p, r);
-                    const int lr = bcast(v0.len, r), o = bcast(off, r);
-                    for (int base = 0; base < lr; base += 64 * 8) {
-                        char x[8];
+                // four rows at a time, so that their loads are in flight
+                // together (one row at a time cost a global round trip per
+                // row before the walk could start)
+                for (int r0 = 0; r0 < n; r0 += 4) {
+                    const char* s4[4];
+                    int l4[4], o4[4], lmax = 0;
 #pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            const int q = base + u * 64 + lane;
-                            x[u] = q < lr ? src[q] : 0;
-                        }
+                    for (int k = 0; k < 4; k++) {
+                        const int r = min(r0 + k, n - 1);
+                        s4[k] = bcast_ptr(v0.p, r);
+                        l4[k] = r0 + k < n ? bcast(v0.len, r) : 0;
+                        o4[k] = bcast(off, r);
+                        lmax = max(lmax, l4[k]);
+                    }
+                    for (int base = 0; base < lmax; base += 64 * 4) {
+                        char x[4][4];
 #pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            const int q = base + u * 64 + lane;
-                            if (q < lr) stage[o + q] = x[u];
-                        }
+                        for (int k = 0; k < 4; k++)
+#pragma unroll
+                            for (int u = 0; u < 4; u++) {
+                                const int q = base + u * 64 + lane;
+                                x[k][u] = q < l4[k] ? s4[k][q] : 0;
+                            }
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+#pragma unroll
+                            for (int u = 0; u < 4; u++) {
+                                const int q = base + u * 64 + lane;
+                                if (q < l4[k]) stage[o4[k] + q] = x[k][u];
+                            }
                     }
                 }
                 __syncthreads();

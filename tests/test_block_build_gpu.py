@@ -190,6 +190,32 @@ def _ou_blocks(rng, n_seqs, seq_len, n_blocks, max_len, self_overlap=False):
     return blocks
 
 
+def test_overlapless_union_many_sequences():
+    """OverlaplessUnion over a consensus-like set: 5000 sequences, about one
+    fragment each plus overlapping clusters and self-overlapping blocks
+    (free_blocks' bucket-by-sequence path), against the oracle."""
+    import numpy as np
+    rng = np.random.default_rng(11)
+    n_seqs, seq_len = 5000, 1200
+    seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
+    names = ["c%d&c&c" % i for i in range(n_seqs)]
+    blocks = _ou_blocks(rng, n_seqs, seq_len, 2500, 600, 40)
+    hot = [int(x) for x in rng.choice(n_seqs, size=20, replace=False)]  # clusters on a few sequences
+    for _ in range(300):
+        s = hot[int(rng.integers(0, len(hot)))]
+        mn = int(rng.integers(0, seq_len - 200))
+        blocks.append([(s, mn, mn + int(rng.integers(10, 200)), 1, None),
+                       (int(rng.integers(0, n_seqs)), 5, 50, -1, None)])
+    ss, eng = _engine(seqs, names)
+    o = orc.BlockSetOracle(seqs, names)
+    eng.set_blocks(blocks).apply("OverlaplessUnion")
+    o.set_blocks(blocks)
+    o.apply("OverlaplessUnion")
+    want = o.blocks()
+    assert eng.blocks() == want
+    assert 0 < len(want) < len(blocks)
+
+
 @pytest.mark.parametrize("max_len,self_overlap", [(40, False), (400, False), (3000, False), (40, True),
                                                   (40, 60), (400, 60), (3000, 60)])
 def test_overlapless_union_many_blocks(max_len, self_overlap):

@@ -12,7 +12,12 @@ for i in $(seq 1 $N); do
 import json, sys
 d = json.loads(open("gpurun_out/ab_%s.log" % sys.argv[1]).read().strip().splitlines()[-1])
 s = d["last_step"]["ms_stage"]
-print(sys.argv[1], d["ms_per_step"], " ".join("%s=%.2f" % (k[:8], v) for k, v in s.items()))
+al = d["last_step"].get("anchor_loop") or {}
+extra = ""
+if al:
+    extra = " | loop " + " ".join("%s=%.2f" % (k[:8], v) for k, v in al["ms_loop"].items()) + " | loop ou=%.2f admit=%.2f" % (
+        al["ms_stage"]["overlapless_union"], al["ms_stage"]["ou_admit"])
+print(sys.argv[1], d["ms_per_step"], " ".join("%s=%.2f" % (k[:8], v) for k, v in s.items()) + extra, flush=True)
 PY
   done
 done

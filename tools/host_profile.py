@@ -2,7 +2,7 @@
 """Host-side sampling profile of the block build (diagnostic; GPU box):
 SIGPROF sampling inside libnpge_amd.so (npge_amd/csrc/host_sampler.cpp)
 during a few DraftPangenome steps; prints the hottest library functions.
-usage: host_profile.py [config] [steps]"""
+usage: host_profile.py [config] [steps] [alf]  (alf: DraftPangenome -> AnchorLoopFast)"""
 import collections
 import ctypes
 import os
@@ -18,7 +18,7 @@ L = _capi.lib()
 _capi.check(L.npgx_set_device(0))
 names, seqs = synth.genome_set(cfg)
 ss = _capi.SeqSet(seqs, names)
-job = pipeline.BlockBuild(ss, names, seqs)
+job = pipeline.BlockBuild(ss, names, seqs, anchor_loop=len(sys.argv) > 3 and sys.argv[3] == "alf")
 job.run()
 out = os.path.abspath("gpurun_out/host_prof_%s.txt" % cfg)
 os.makedirs(os.path.dirname(out), exist_ok=True)

@@ -1251,6 +1251,10 @@ __global__ __launch_bounds__(64 * SPLIT_WAVES) void k_split_find(SaArgs a, const
 
 // ---------------------------------------------------- split jobs after their segments
 static constexpr int POST_THREADS = 256;
+// k_split_post's workgroup: FindLowSimilar's region rounds over a whole-genome
+// chain (tens of thousands of regions in global memory) are bound by the
+// elements each thread walks per round
+static constexpr int REG_THREADS = 1024;
 static constexpr int FIN_PARTS = 16;  // workgroups assembling one deferred job's B
 static constexpr size_t POST_LDS = 144 * 1024;
 
@@ -1273,8 +1277,8 @@ __device__ __forceinline__ int block_scan_excl(int v, int* total, int* scratch4)
     if (lane == 63) scratch4[wid] = inc;
     __syncthreads();
     int before = 0, all = 0;
-#pragma unroll
-    for (int q = 0; q < POST_THREADS / 64; q++) {
+    const int nwv = (int)blockDim.x >> 6;  // (POST_THREADS or REG_THREADS)
+    for (int q = 0; q < nwv; q++) {
         const int s = scratch4[q];
         before += q < wid ? s : 0;
         all += s;
@@ -1302,7 +1306,7 @@ __device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long 
     const int tid = threadIdx.x;
     // region starts: where the identical bit flips (and column 0)
     int cnt = 0;
-    for (int q = tid; q < nw; q += POST_THREADS) {
+    for (int q = tid; q < nw; q += (int)blockDim.x) {
         const unsigned long long g = gm[q];
         const unsigned long long valid = (q < nw - 1 || (L & 63) == 0) ? ~0ull : ((1ull << (L & 63)) - 1);
         unsigned long long st = (g ^ ((g << 1) | (q > 0 ? (gm[q - 1] >> 63) : (g & 1ull)))) & valid;
@@ -1321,7 +1325,7 @@ __device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long 
     unsigned char* mf = (unsigned char*)(qw + R);  // this round's merging regions
     // starts in order: words dealt out in contiguous runs per thread
     {
-        const int per = (nw + POST_THREADS - 1) / POST_THREADS;
+        const int per = (nw + (int)blockDim.x - 1) / (int)blockDim.x;
         const int q0 = min(nw, tid * per), q1 = min(nw, q0 + per);
         int c = 0;
         for (int q = q0; q < q1; q++) {
@@ -1348,7 +1352,7 @@ __device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long 
     }
     __syncthreads();
     const int WM = 0x7fffffff;
-    for (int i = tid; i < R; i += POST_THREADS) {  // Region::set_weight :48-54
+    for (int i = tid; i < R; i += (int)blockDim.x) {  // Region::set_weight :48-54
         const int len = (i + 1 < R ? rx[i + 1] : L) - rx[i];
         const int good = (int)((unsigned)rw[i] >> 31);
         rw[i] = (good << 31) | (good ? len : len * wf);
@@ -1359,7 +1363,7 @@ __device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long 
         if (tid == 0) s_any = 0;
         __syncthreads();
         int any = 0;
-        for (int i = tid; i < R; i += POST_THREADS) {
+        for (int i = tid; i < R; i += (int)blockDim.x) {
             const int wi = rw[i] & WM;
             bool m = wi < min_length;
             for (int d = -2; d <= 2 && m; d++) {
@@ -1376,7 +1380,7 @@ __device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long 
         if (!s_any) break;
         // merge (merge_region :94-119) and compact into the other copy: every
         // thread a contiguous run of regions, one scan for the new places
-        const int C = (R + POST_THREADS - 1) / POST_THREADS;
+        const int C = (R + (int)blockDim.x - 1) / (int)blockDim.x;
         const int i0 = min(R, tid * C), i1 = min(R, i0 + C);
         int kept = 0;
         for (int i = i0; i < i1; i++) kept += !((i > 0 && mf[i - 1]) || (i + 1 < R && mf[i + 1]));
@@ -1409,7 +1413,7 @@ __device__ int regions_block(G* gm, int nw, int L, int wf, int min_length, long 
     }
     if (R > out_cap) return -1;
     // survivors with their identical columns (score_of before re-alignment)
-    for (int i = tid; i < R; i += POST_THREADS) {
+    for (int i = tid; i < R; i += (int)blockDim.x) {
         const int x = rx[i], y = (i + 1 < R ? rx[i + 1] : L) - 1;
         const int good = (int)((unsigned)rw[i] >> 31);
         int c = 0;
@@ -1543,13 +1547,13 @@ __global__ __launch_bounds__(POST_THREADS) void k_chain_copy(SaArgs a, int n_spl
 }
 
 struct PostShared {
-    int np, L0, fail, R, scan[POST_THREADS / 64];
+    int np, L0, fail, R, scan[REG_THREADS / 64];
 };
 
 template <class G, class I>
 __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long long area_bytes, PostShared& ps);
 
-__global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_bytes) {
+__global__ __launch_bounds__(REG_THREADS) void k_split_post(SaArgs a, int lds_bytes) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_p[];
     __shared__ PostShared ps;
     const int tid = threadIdx.x, si = blockIdx.x;
@@ -1572,7 +1576,7 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_post(SaArgs a, int lds_b
     LdsU64w* gm = (LdsU64w*)lds_p;
     if (!hd.z && (long long)nw * 16 <= lds_bytes) {
         const unsigned long long* gb = a.chain_bits + a.bits_off[si];
-        for (int q = tid; q < nw; q += POST_THREADS) gm[q] = gb[q];
+        for (int q = tid; q < nw; q += (int)blockDim.x) gm[q] = gb[q];
     }
     __syncthreads();
     split_post_body<LdsU64w, LdsInt>(a, sp, gm, lds_bytes, ps);
@@ -2939,7 +2943,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
             ti = al->timer.begin("align_split_post", st, 0.0, (int64_t)splits.size());
-            hipLaunchKernelGGL(k_split_post, dim3((unsigned)splits.size()), dim3(POST_THREADS), POST_LDS, st, A,
+            hipLaunchKernelGGL(k_split_post, dim3((unsigned)splits.size()), dim3(REG_THREADS), POST_LDS, st, A,
                                (int)POST_LDS);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);

@@ -1255,7 +1255,7 @@ static constexpr int POST_THREADS = 256;
 // chain (tens of thousands of regions in global memory) are bound by the
 // elements each thread walks per round
 static constexpr int REG_THREADS = 1024;
-static constexpr int FIN_PARTS = 16;  // workgroups assembling one deferred job's B
+static constexpr int FIN_PARTS = 64;  // workgroups assembling one deferred job's B
 static constexpr size_t POST_LDS = 144 * 1024;
 
 __device__ __forceinline__ long long wave_sum64(long long v) {
@@ -1858,15 +1858,49 @@ __global__ __launch_bounds__(POST_THREADS) void k_sub_post(SaArgs a, int first) 
     }
 }
 
+// k_fin_prefix: per deferred job (one workgroup of REG_THREADS each), the
+// output offset of every region in B (g_dst[reg_off + j ..], R + 1 values;
+// the last = B's length, or -1 when a re-alignment overflowed or B would
+// not fit) -- once, for all of k_fin_copy's parts (each part scanned every
+// region itself: serial in the region count of whole-genome jobs)
+__global__ __launch_bounds__(REG_THREADS) void k_fin_prefix(SaArgs a, int* g_dst) {
+    __shared__ int scan[REG_THREADS / 64];
+    __shared__ int s_bad;
+    const int fn = blockIdx.x;
+    if (fn >= (int)a.counters[1]) return;
+    const int tid = threadIdx.x;
+    const int j = a.fin[fn];
+    const SaJob job = a.jobs[j];
+    const int R = a.job_nreg[j];
+    const int4* jr = a.job_regions + job.reg_off;
+    int* dst = g_dst + job.reg_off + j;
+    if (tid == 0) {
+        dst[0] = 0;
+        s_bad = 0;
+    }
+    int carry = 0, bad = 0;
+    for (int c0 = 0; c0 < R; c0 += REG_THREADS) {
+        const int ri = c0 + tid;
+        const int wd = ri < R ? fin_width(a, jr[ri]) : 0;
+        bad |= wd < 0;
+        int tot = 0;
+        const int pre = block_scan_excl(max(wd, 0), &tot, scan);
+        if (ri < R) dst[ri + 1] = carry + pre + max(wd, 0);
+        carry += tot;
+    }
+    if (bad) s_bad = 1;
+    __syncthreads();
+    if (tid == 0) dst[R] = (s_bad || carry > job.cap) ? -1 : carry;  // k_align_finish marks the overflow
+}
+
 // k_fin_copy: B of every deferred job, FIN_PARTS workgroups per job, each a
-// range of B's columns; column c of B comes from the region whose output
-// offsets hold it (binary search over the offsets in LDS)
+// share of B's columns (the region offsets from k_fin_prefix, into LDS when
+// they fit)
 __global__ __launch_bounds__(POST_THREADS) void k_fin_copy(SaArgs a, int lds_ints, int* g_dst) {
     extern __shared__ __attribute__((aligned(16))) int dst_l[];
-    __shared__ int s_tot;
     const int fn = blockIdx.x / FIN_PARTS, part = blockIdx.x % FIN_PARTS;
     if (fn >= (int)a.counters[1]) return;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     const int j = a.fin[fn];
     const SaJob job = a.jobs[j];
     const int n = job.n, cap = job.cap;
@@ -1874,31 +1908,15 @@ __global__ __launch_bounds__(POST_THREADS) void k_fin_copy(SaArgs a, int lds_int
     char* B = (char*)A + (size_t)n * cap;
     const int R = a.job_nreg[j];
     const int4* jr = a.job_regions + job.reg_off;
-    // output offsets (every part computes them; the global fallback is
-    // written with equal values by every part of the job)
-    int* dst = R + 1 <= lds_ints ? dst_l : g_dst + job.reg_off + j;
-    if (tid < 64) {
-        int carry = 0, bad = 0;
-        if (lane == 0) dst[0] = 0;
-        for (int c0 = 0; c0 < R; c0 += 64) {
-            const int ri = c0 + lane;
-            const int wd = ri < R ? fin_width(a, jr[ri]) : 0;
-            bad |= wd < 0;
-            int pre = max(wd, 0);
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(pre, o);
-                if (lane >= o) pre += t;
-            }
-            if (ri < R) dst[ri + 1] = carry + pre;
-            carry += __shfl(pre, 63);
-        }
-        bad = (int)(ballot(bad) != 0);
-        if (lane == 0) s_tot = (bad || carry > cap) ? -1 : carry;  // k_align_finish marks the overflow
-    }
-    __syncthreads();
-    const int tot = s_tot;
+    const int* gd = g_dst + job.reg_off + j;
+    const int tot = gd[R];
     if (tot <= 0) return;
+    const int* dst = gd;
+    if (R + 1 <= lds_ints) {
+        for (int i = tid; i <= R; i += POST_THREADS) dst_l[i] = gd[i];
+        __syncthreads();
+        dst = dst_l;
+    }
     const int c0 = (int)((int64_t)tot * part / FIN_PARTS), c1 = (int)((int64_t)tot * (part + 1) / FIN_PARTS);
     for (int c = c0 + tid; c < c1; c += POST_THREADS) {
         int lo = 0, hi = R - 1;  // the region ri with dst[ri] <= c < dst[ri+1]
@@ -2991,6 +3009,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             }
             if (n_fin > 0) {
                 ti = al->timer.begin("align_fin_copy", st, 0.0, 0);
+                hipLaunchKernelGGL(k_fin_prefix, dim3((unsigned)n_fin), dim3(REG_THREADS), 0, st, A, al->d_reg_dst.p);
+                NPGX_HIP(hipGetLastError());
                 hipLaunchKernelGGL(k_fin_copy, dim3((unsigned)(n_fin * FIN_PARTS)), dim3(POST_THREADS),
                                    (size_t)lds_ints * 4, st, A, lds_ints, al->d_reg_dst.p);
                 NPGX_HIP(hipGetLastError());

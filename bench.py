@@ -13,7 +13,12 @@ every N so that the per-N values compare:
     own RCCL communicator over xGMI (npge_amd/comm.py RcclComm) -- strong
     scaling; value = that set's bp / time;
   --mode replicas: every rank processes its own genome set (same config,
-    rank-specific seed), no data-path collective -- weak scaling.
+    rank-specific seed), no data-path collective -- weak scaling;
+  --mode pairs (BASELINE C4's split; default config C4): every genome pair of
+    the set is one DraftPangenome, the pairs split round-robin over the ranks
+    and run --pair-workers at a time per GPU, RCCL only for the final gather
+    of every pair's blocks (npge_amd/pairs.py) -- strong scaling over the
+    fixed pair job; value = all pairs' input bp / time.
 With N > 1 and --mode sharded the line also carries "replicas": the same
 step measured in replica mode right after, for the throughput of N
 independent sets.
@@ -37,10 +42,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C3",
-                    help="synthetic genome set (npge_amd/synth.py); C3 = the 17-genome ≥50x target config")
-    ap.add_argument("--mode", choices=("replicas", "sharded"), default="sharded",
-                    help="N > 1: sharded (one set over the ranks, strong scaling; default) or replicas")
+    ap.add_argument("--config", default=None,
+                    help="synthetic genome set (npge_amd/synth.py); default C3 = the 17-genome ≥50x target "
+                         "config (C4 with --mode pairs)")
+    ap.add_argument("--mode", choices=("replicas", "sharded", "pairs"), default="sharded",
+                    help="N > 1: sharded (one set over the ranks, strong scaling; default), replicas, "
+                         "or pairs (genome pairs over the ranks, any N)")
+    ap.add_argument("--pair-workers", type=int, default=4, help="--mode pairs: pairs run at a time per GPU")
+    ap.add_argument("--pairs", type=int, default=0, help="--mode pairs: the first P pairs only (0 = all)")
     ap.add_argument("--no-replicas-line", action="store_true",
                     help="N > 1 sharded: skip the secondary replica-mode measurement")
     ap.add_argument("--anchor-loop", action="store_true",
@@ -50,7 +59,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default=None, help="synthetic config timed for cpu_baseline (default: --config)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU runs (median) after one warm-up")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config is None:
+        a.config = "C4" if a.mode == "pairs" else "C3"
+    return a
 
 
 def main():
@@ -74,6 +86,8 @@ def main():
     from npge_amd import pipeline
 
     _capi.check(_capi.lib().npgx_set_device(local_rank))
+    if args.mode == "pairs":
+        return main_pairs(args, dist, world, rank, local_rank)
     sharded = args.mode == "sharded" and world > 1
     seed = harness.rank_seed(synth.BASE_SEED, 0 if sharded else rank, args.config)
     names, seqs = synth.genome_set(args.config, seed=seed)
@@ -189,6 +203,106 @@ def main():
             del job
             comm.close()
         dist.destroy_process_group()
+
+
+def main_pairs(args, dist, world, rank, local_rank):
+    """--mode pairs: the pair-sharded job (npge_amd/pairs.py).  One step = every
+    pair of the set through DraftPangenome once (the rank's share, --pair-workers
+    at a time) + the final all-gather of every pair's blocks."""
+    import torch
+    from npge_amd import comm as ncomm, harness, pairs, synth
+    names, seqs = synth.genome_set(args.config)
+    sel = pairs.all_pairs(names)
+    if args.pairs:
+        sel = sel[:args.pairs]
+    comm = None
+    if world > 1:
+        if args.dist_backend == "nccl":
+            comm = ncomm.RcclComm(dist, local_rank)
+        else:
+            comm = ncomm.TorchComm(dist, staging="cpu")
+        ncomm.check(comm)
+    gdev = torch.device("cuda", local_rank) if world > 1 and args.dist_backend == "nccl" else None
+    job = pairs.PairJobs(names, seqs, rank=rank, world=world, comm=comm, workers=args.pair_workers,
+                         pairs=sel, device=local_rank, gather_device=gdev)
+    torch.cuda.synchronize()
+    dt, info = harness.timed_steps(job.run, args.steps, args.warmup, dist if world > 1 else None,
+                                   sync=torch.cuda.synchronize, device="cuda")
+    total = job.total_bp()
+    value = total * args.steps / dt / 1e6          # the whole pair job over the max-over-ranks time
+    agg = {}
+    for _, _, bb in job.jobs:
+        for k in bb.kernel_times():
+            a = agg.setdefault(k["name"], {"name": k["name"], "ms": 0.0, "bytes": 0.0, "launches": 0})
+            a["ms"] += k["ms"]
+            a["bytes"] += k["bytes"]
+            a["launches"] += k["launches"]
+    kern = [k for k in agg.values() if not k["name"].endswith("_allreduce")]
+    dom = max(kern, key=lambda k: k["ms"]) if kern else None
+    roofline = None
+    if dom and dom["ms"] > 0:
+        ach = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "kernel": dom["name"],
+                    "launches_per_rank_step": dom["launches"],
+                    "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
+                    "bytes_per_launch": dom["bytes"] / dom["launches"],
+                    "note": "kernel times summed over the rank's pairs (concurrent streams overlap)"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_pair(names, seqs, sel[0], args.cpu_runs)
+    if rank == 0:
+        line = {
+            "metric": "anchored+aligned Mbp/sec at 1/2/4/8 MI355X; bit-exact anchor set vs CPU",
+            "value": round(value, 3), "unit": "Mbp/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded, npge_amd/synth.py)",
+            "config": {"workload": "%s pair-sharded: DraftPangenome per genome pair (%d pairs, %d bp), "
+                                   "final all-gather of every pair's blocks" % (args.config, len(sel), total),
+                       "genomes": synth.CONFIGS[args.config][0], "pairs": len(sel), "bp_job": total,
+                       "pair_workers": args.pair_workers,
+                       "inputs": "every pair's sequences resident in HBM before the timed region",
+                       "parallelism": "pairs round-robin over %d rank(s); %s" % (
+                           world, "library RCCL communicator" if comm is not None and args.dist_backend == "nccl"
+                           else (args.dist_backend if world > 1 else "no collective"))},
+            "last_step": info,
+            "device_mem_used_gb": round((lambda f: (f[1] - f[0]) / 2**30)(torch.cuda.mem_get_info()), 2),
+            "kernels_last_step": sorted(({"name": k["name"], "ms": round(k["ms"], 4), "launches": k["launches"]}
+                                         for k in agg.values()), key=lambda k: -k["ms"])[:12],
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        del job
+        if comm is not None and hasattr(comm, "close"):
+            comm.close()
+        dist.destroy_process_group()
+
+
+def cpu_baseline_pair(names, seqs, idx, runs):
+    """The oracle's DraftPangenome on one genome pair of the job (a bounded
+    sample of the pair workload), one thread, median of `runs` after a warm-up."""
+    import statistics
+    import time
+    from oracle import oracle as orc
+    native = orc.use_native()
+    pn, ps = [names[i] for i in idx], [seqs[i] for i in idx]
+    bp = sum(len(s) for s in ps)
+    ts = []
+    for r in range(runs + 1):
+        o = orc.BlockSetOracle(ps, pn, seed=1)
+        t = time.perf_counter()
+        o.apply("DraftPangenome")
+        if r:
+            ts.append(time.perf_counter() - t)
+    t1 = statistics.median(ts)
+    return {"value": round(bp / 1e6 / t1, 4), "unit": "Mbp/s", "cores": 1, "kind": "port",
+            "sample": "one genome pair of the job (%s, %d bp), DraftPangenome, oracle/ C++ %s, 1 thread, "
+                      "median of %d runs after 1 warm-up" % ("+".join(pn), bp,
+                                                            "-O3 -march=native" if native else "-O3", runs),
+            "workload": "DraftPangenome", "seconds": round(t1, 3), "host": _cpu_info()}
 
 
 def pmc_traffic(kernel, config):

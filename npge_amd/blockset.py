@@ -168,6 +168,22 @@ class BlockSetEngine:
             out.append(blk)
         return out
 
+    def fragments(self):
+        """Fragment coordinates without rows (no row download): numpy arrays
+        (block_start[nb + 1], seq, min, max, ori) in block order."""
+        L = _capi.lib()
+        nb, nf, rb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _capi.check(L.npgx_blockset_counts(self._h, ctypes.byref(nb), ctypes.byref(nf), ctypes.byref(rb)))
+        n = max(nf.value, 1)
+        bs = np.zeros(nb.value + 1, dtype=np.int64)
+        seq = np.zeros(n, dtype=np.int32)
+        mn = np.zeros(n, dtype=np.int64)
+        mx = np.zeros(n, dtype=np.int64)
+        ori = np.zeros(n, dtype=np.int8)
+        _capi.check(L.npgx_blockset_copy(self._h, _capi.ptr(bs), _capi.ptr(seq), _capi.ptr(mn),
+                                         _capi.ptr(mx), _capi.ptr(ori), None, None))
+        return bs, seq[:nf.value], mn[:nf.value], mx[:nf.value], ori[:nf.value]
+
     def conseq(self):
         """ConSeq (ConSeq.cpp:37-50): the text of the sequence each block
         becomes, in block order (consensus of aligned blocks on the GPU)."""

@@ -1,0 +1,218 @@
+"""Pair-sharded block build: the north star's multi-GPU split for BASELINE
+config C4 ("32 genomes x 5 Mbp, 2 % divergence, pair-sharded across
+8 x MI355X with RCCL gather"; DESIGN.md "Multi-GPU").
+
+The unit is a genome pair.  Every pair (i < j) of the set's genomes is one
+independent DraftPangenome (lua_lib.lua:1569-1621) over the two genomes'
+sequences -- the same call the reference's `npge` runs on a two-genome input,
+so each pair's blocks are bit-exact with the CPU path on that pair
+(tests/test_pairs_gpu.py against oracle/).  Pairs go to ranks round-robin in
+pair order (all pairs of a config have about the same size); on its GPU a
+rank runs `workers` pairs at a time, each on its own host thread with its own
+sequence set, block set, aligner and AnchorFinder handle (one HIP stream
+each), so that the latency-bound iterations of one pair overlap the others'.
+The data path has no collective until the end: every rank's anchored+aligned
+blocks -- fragment coordinates per pair -- are all-gathered once over the
+communicator (RCCL over xGMI on the GPU box: the library's own npgx_comm), so
+every rank ends with the whole job's block sets.
+
+Host-side pieces (pair list, assignment, record packing, the gather over an
+npgx_comm) use no GPU call and are tested on CPU with gloo
+(tests/test_pairs_dist.py).
+"""
+import ctypes
+import itertools
+import threading
+import time
+
+import numpy as np
+
+# record layout of one fragment (2 x u64):
+#   w0 = pair << 44 | block << 4 | local_seq << 1 | (ori > 0)
+#   w1 = min << 32 | max
+PAIR_BITS, BLOCK_BITS, SEQ_BITS = 20, 40, 3
+# per-pair summary record (2 x u64): (pair << 32 | n_blocks), blockset hash
+
+
+def genomes_of(names):
+    """Genome of each sequence by its name (Sequence::genome, Sequence.cpp:193-202:
+    the part before the first '&'), in first-seen order -> {genome: [seq index]}."""
+    out = {}
+    for i, n in enumerate(names):
+        out.setdefault(n.split("&", 1)[0], []).append(i)
+    return out
+
+
+def all_pairs(names):
+    """Every pair (i < j) of the set's genomes, in order: [(seq indices of the pair)]."""
+    g = list(genomes_of(names).values())
+    return [tuple(g[a] + g[b]) for a, b in itertools.combinations(range(len(g)), 2)]
+
+
+def assign(n_pairs, rank, world):
+    """Pair indices of `rank`: round-robin in pair order."""
+    return list(range(rank, n_pairs, world))
+
+
+def pack_fragments(pair, bs, seq, mn, mx, ori):
+    """Fragment records of one pair's block set (npgx_blockset_copy arrays)."""
+    nb = len(bs) - 1
+    nf = int(bs[-1]) if nb >= 0 else 0
+    if nf == 0:
+        return np.zeros(0, dtype=np.uint64)
+    assert pair < (1 << PAIR_BITS) and nb < (1 << BLOCK_BITS)
+    assert int(seq[:nf].max()) < (1 << SEQ_BITS) and int(mx[:nf].max()) < (1 << 32)
+    blk = np.repeat(np.arange(nb, dtype=np.uint64), np.diff(bs).astype(np.int64))
+    w0 = ((np.uint64(pair) << np.uint64(44)) | (blk << np.uint64(4))
+          | (seq[:nf].astype(np.uint64) << np.uint64(1)) | (ori[:nf] > 0).astype(np.uint64))
+    w1 = (mn[:nf].astype(np.uint64) << np.uint64(32)) | mx[:nf].astype(np.uint64)
+    return np.stack([w0, w1], axis=1).reshape(-1)
+
+
+def unpack_fragments(rec):
+    """-> {pair: [[(local_seq, min, max, ori), ...] per block]} (blocks in their order)."""
+    r = rec.reshape(-1, 2)
+    out = {}
+    for w0, w1 in r.tolist():
+        p, b = w0 >> 44, (w0 >> 4) & ((1 << BLOCK_BITS) - 1)
+        blocks = out.setdefault(p, [])
+        while len(blocks) <= b:
+            blocks.append([])
+        blocks[b].append(((w0 >> 1) & 7, w1 >> 32, w1 & 0xffffffff, 1 if w0 & 1 else -1))
+    return out
+
+
+def _struct(comm):
+    from .comm import NpgxComm, TorchComm
+    if isinstance(comm, TorchComm):
+        return comm.struct
+    return ctypes.cast(comm.pointer(), ctypes.POINTER(NpgxComm)).contents
+
+
+def gather_u64(comm, arr, device=None):
+    """All-gather of a variable-length u64 array over an npgx_comm (rank
+    order): allgather_i64 of the counts, then one allgatherv_u64.  device: a
+    torch device for the exchange buffers (RCCL needs device memory); None
+    passes host arrays (gloo TorchComm with host staging, CPU tests)."""
+    c = _struct(comm)
+    world = c.world
+    counts = (ctypes.c_int64 * world)()
+    if c.allgather_i64(c.user, int(len(arr)), counts) != 0:
+        raise RuntimeError("allgather_i64 failed")
+    tot = sum(counts)
+    if tot == 0:
+        return np.zeros(0, dtype=np.uint64), list(counts)
+    arr = np.ascontiguousarray(arr, dtype=np.uint64)
+    if device is None:
+        src = arr if len(arr) else np.zeros(1, dtype=np.uint64)
+        dst = np.zeros(tot, dtype=np.uint64)
+        rc = c.allgatherv_u64(c.user, src.ctypes.data, counts, dst.ctypes.data)
+        out = dst
+    else:
+        import torch
+        src = torch.from_numpy(arr.view(np.int64) if len(arr) else np.zeros(1, dtype=np.int64)).to(device)
+        dst = torch.empty(tot, dtype=torch.int64, device=device)
+        torch.cuda.synchronize(device)
+        rc = c.allgatherv_u64(c.user, src.data_ptr(), counts, dst.data_ptr())
+        out = dst.cpu().numpy().view(np.uint64)
+    if rc != 0:
+        raise RuntimeError("allgatherv_u64 failed")
+    return out, list(counts)
+
+
+class PairJobs:
+    """The rank's share of the pair-sharded job: its pairs resident in HBM (one
+    sequence set + block set + AnchorFinder handle per pair, made before any
+    timing), run `workers` at a time; run() = one pass over the rank's pairs
+    plus the final gather."""
+
+    def __init__(self, names, seqs, rank=0, world=1, comm=None, workers=4, pairs=None, device=0,
+                 gather_device=None):
+        from . import _capi
+        from .pipeline import BlockBuild
+        self.pairs = all_pairs(names) if pairs is None else list(pairs)
+        self.mine = assign(len(self.pairs), rank, world)
+        self.comm = comm
+        self.workers = max(1, int(workers))
+        self.device = device
+        self.gather_device = gather_device
+        self.pair_bp = [sum(len(seqs[i]) for i in self.pairs[p]) for p in range(len(self.pairs))]
+        self.jobs = []
+        for p in self.mine:
+            idx = self.pairs[p]
+            pn, ps = [names[i] for i in idx], [seqs[i] for i in idx]
+            ss = _capi.SeqSet(ps, pn)
+            self.jobs.append((p, ss, BlockBuild(ss, pn, ps)))
+        self.records = None
+        self.summary = None
+
+    def total_bp(self):
+        """Input bp of the whole job (all ranks' pairs)."""
+        return sum(self.pair_bp)
+
+    def rank_bp(self):
+        return sum(self.pair_bp[p] for p, _, _ in self.jobs)
+
+    def _run_pairs(self):
+        from . import _capi
+        nxt = iter(range(len(self.jobs)))
+        lock = threading.Lock()
+        infos = [None] * len(self.jobs)
+        errors = []
+
+        def worker():
+            try:
+                _capi.check(_capi.lib().npgx_set_device(self.device))
+                while True:
+                    with lock:
+                        k = next(nxt, None)
+                    if k is None or errors:
+                        return
+                    infos[k] = self.jobs[k][2].run()
+            except Exception as e:  # re-raised on the calling thread
+                errors.append(e)
+
+        n = min(self.workers, len(self.jobs))
+        if n <= 1:
+            worker()
+        else:
+            ts = [threading.Thread(target=worker) for _ in range(n)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+        if errors:
+            raise errors[0]
+        return infos
+
+    def local_records(self):
+        frs, sums = [], []
+        for p, _, job in self.jobs:
+            bs, seq, mn, mx, ori = job.eng.fragments()
+            frs.append(pack_fragments(p, bs, seq, mn, mx, ori))
+            sums.append(np.array([(p << 32) | (len(bs) - 1), job.eng.hash()], dtype=np.uint64))
+        cat = (lambda a: np.concatenate(a) if a else np.zeros(0, dtype=np.uint64))
+        return cat(frs), cat(sums)
+
+    def run(self):
+        t0 = time.perf_counter()
+        infos = self._run_pairs()
+        t1 = time.perf_counter()
+        frs, sums = self.local_records()
+        if self.comm is not None:  # the one collective: the final anchored-block gather
+            frs, _ = gather_u64(self.comm, frs, self.gather_device)
+            sums, _ = gather_u64(self.comm, sums, self.gather_device)
+        self.records, self.summary = frs, sums
+        t2 = time.perf_counter()
+        done = [i for i in infos if i is not None]
+        return {"pairs": len(self.pairs), "pairs_rank": len(self.jobs), "workers": self.workers,
+                "ms_pairs": round((t1 - t0) * 1e3, 3), "ms_gather": round((t2 - t1) * 1e3, 3),
+                "gathered_fragments": int(len(frs) // 2), "gathered_pairs": int(len(sums) // 2),
+                "stem_blocks": int(sum(i["stem_blocks"] for i in done)),
+                "aligned_residues": int(sum(i["aligned_residues"] for i in done)),
+                "align_jobs": int(sum(i["align_jobs"] for i in done))}
+
+    def hashes(self):
+        """{pair: blockset hash} of the gathered summaries (after run())."""
+        s = self.summary.reshape(-1, 2)
+        return {int(a >> 32): int(h) for a, h in s.tolist()}

@@ -8,21 +8,21 @@ value = input bp of all ranks / max-over-ranks wall time of the K timed steps.
 
 Multi-GPU (torch.distributed.run, one rank per GPU), the same workload at
 every N so that the per-N values compare:
-  --mode sharded (default for N > 1): ONE genome set, the AnchorFinder windows
-    and the aligner jobs split over the ranks, the exchanges on the library's
-    own RCCL communicator over xGMI (npge_amd/comm.py RcclComm) -- strong
-    scaling; value = that set's bp / time;
-  --mode replicas: every rank processes its own genome set (same config,
-    rank-specific seed), no data-path collective -- weak scaling;
+  --mode replicas (default): every rank processes its own genome set of the
+    config (rank-specific seed) -- independent pangenome jobs, no data-path
+    collective, weak scaling; value = all ranks' bp / max-over-ranks time;
+  --mode sharded: ONE genome set, the AnchorFinder windows and the aligner
+    jobs split over the ranks, the exchanges on the library's own RCCL
+    communicator over xGMI (npge_amd/comm.py RcclComm) -- strong scaling;
   --mode pairs (BASELINE C4's split; default config C4): every genome pair of
     the set is one DraftPangenome, the pairs split round-robin over the ranks
     and run --pair-workers at a time per GPU, RCCL only for the final gather
     of every pair's blocks (npge_amd/pairs.py) -- strong scaling over the
     fixed pair job; value = all pairs' input bp / time.
-With N > 1 and --mode sharded the line also carries "replicas": the same
-step measured in replica mode right after, for the throughput of N
-independent sets.
-(DESIGN.md "Multi-GPU").
+Every line also carries, each timed on its own after the headline:
+"sharded" (N > 1: one set over the ranks; with --mode sharded "replicas"
+instead) and "pairs" (the C4 pair-sharded job at this N), so one SCALE run
+gives all three curves.  (DESIGN.md "Multi-GPU").
 
 Prints ONE JSON line on rank 0.
 """
@@ -45,13 +45,16 @@ def parse():
     ap.add_argument("--config", default=None,
                     help="synthetic genome set (npge_amd/synth.py); default C3 = the 17-genome ≥50x target "
                          "config (C4 with --mode pairs)")
-    ap.add_argument("--mode", choices=("replicas", "sharded", "pairs"), default="sharded",
-                    help="N > 1: sharded (one set over the ranks, strong scaling; default), replicas, "
-                         "or pairs (genome pairs over the ranks, any N)")
-    ap.add_argument("--pair-workers", type=int, default=4, help="--mode pairs: pairs run at a time per GPU")
-    ap.add_argument("--pairs", type=int, default=0, help="--mode pairs: the first P pairs only (0 = all)")
+    ap.add_argument("--mode", choices=("replicas", "sharded", "pairs"), default="replicas",
+                    help="replicas (every rank its own set, weak scaling; default), sharded (one set over "
+                         "the ranks, strong scaling) or pairs (C4 genome pairs over the ranks)")
+    ap.add_argument("--pair-workers", type=int, default=12, help="pairs: pairs run at a time per GPU")
+    ap.add_argument("--pairs", type=int, default=0, help="pairs: the first P pairs only (0 = all)")
     ap.add_argument("--no-replicas-line", action="store_true",
-                    help="N > 1 sharded: skip the secondary replica-mode measurement")
+                    help="N > 1: skip the secondary one-set (or, with --mode sharded, replica) measurement")
+    ap.add_argument("--pairs-config", default="C4", help="the secondary pairs line's config")
+    ap.add_argument("--no-pairs-line", action="store_true",
+                    help="skip the secondary C4 pair-sharded measurement")
     ap.add_argument("--anchor-loop", action="store_true",
                     help="each step also runs one AnchorLoopFast after DraftPangenome (lua_lib.lua:741-758)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -86,22 +89,27 @@ def main():
     from npge_amd import pipeline
 
     _capi.check(_capi.lib().npgx_set_device(local_rank))
-    if args.mode == "pairs":
-        return main_pairs(args, dist, world, rank, local_rank)
-    sharded = args.mode == "sharded" and world > 1
-    seed = harness.rank_seed(synth.BASE_SEED, 0 if sharded else rank, args.config)
-    names, seqs = synth.genome_set(args.config, seed=seed)
-    bp = synth.total_bp(seqs)
-    ss = _capi.SeqSet(seqs, names)          # resident in HBM before timing
     comm = None
-    if sharded:
+    if world > 1:  # one communicator for the sharded set and the pair gather
         from npge_amd import comm as ncomm
         if args.dist_backend == "nccl":
             comm = ncomm.RcclComm(dist, local_rank)  # the library's own RCCL communicator
         else:  # gloo rehearsal: ranks may share a GPU (RCCL refuses that)
             comm = ncomm.TorchComm(dist, staging="cpu")
         ncomm.check(comm)  # every collective once, results verified, before any timing
-    job = pipeline.BlockBuild(ss, names, seqs, comm=comm, anchor_loop=args.anchor_loop)
+    if args.mode == "pairs":
+        line = run_pairs(args, dist, world, rank, local_rank, comm, args.config, args.pairs,
+                         args.steps, args.warmup, baseline=not args.no_cpu_baseline)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        finish(dist, world, comm)
+        return
+    sharded = args.mode == "sharded" and world > 1
+    seed = harness.rank_seed(synth.BASE_SEED, 0 if sharded else rank, args.config)
+    names, seqs = synth.genome_set(args.config, seed=seed)
+    bp = synth.total_bp(seqs)
+    ss = _capi.SeqSet(seqs, names)          # resident in HBM before timing
+    job = pipeline.BlockBuild(ss, names, seqs, comm=comm if sharded else None, anchor_loop=args.anchor_loop)
 
     def step():
         return job.run()
@@ -110,19 +118,6 @@ def main():
                                    sync=torch.cuda.synchronize, device="cuda")
     # sharded: the ranks share one set of bp; replicas: each rank has its own
     value = harness.throughput(bp, 1 if sharded else world, args.steps, dt) / 1e6
-    replicas = None
-    if sharded and not args.no_replicas_line:
-        # secondary line: the same step in replica mode (every rank its own set, no collective)
-        rseed = harness.rank_seed(synth.BASE_SEED, rank, args.config)
-        rnames, rseqs = synth.genome_set(args.config, seed=rseed)
-        rss = _capi.SeqSet(rseqs, rnames)
-        rjob = pipeline.BlockBuild(rss, rnames, rseqs, anchor_loop=args.anchor_loop)
-        rdt, _ = harness.timed_steps(rjob.run, args.steps, args.warmup, dist,
-                                     sync=torch.cuda.synchronize, device="cuda")
-        replicas = {"value": round(harness.throughput(synth.total_bp(rseqs), world, args.steps, rdt) / 1e6, 3),
-                    "unit": "Mbp/s", "ms_per_step": round(rdt / args.steps * 1e3, 4), "scaling": "weak",
-                    "parallelism": "replica-per-gpu x%d (independent sets, no collective)" % world}
-        del rjob, rss
 
     # dominant kernel of the last step: algorithmic bytes / HIP-event duration
     # (events recorded on the engine's own stream around each launch)
@@ -143,6 +138,8 @@ def main():
 
     if roofline is not None:
         roofline.update(pmc_traffic(dom["name"], args.config))
+    workload = job.workload_name(args.config)
+    del job
 
     # the boundary takes host buffers: time the upload (to_atgcn + H2D + pack,
     # npgx_seqset_create) on its own; `value` excludes it (inputs resident in
@@ -161,6 +158,37 @@ def main():
     step_s = dt / args.steps
     pcie = {"upload_ms": round(up * 1e3, 3),
             "value": round(harness.throughput(bp, 1 if sharded else world, 1, step_s + up) / 1e6, 3)}
+
+    # secondary lines, each in its own timed region after the headline's
+    other = None
+    if world > 1 and not args.no_replicas_line:
+        if sharded:  # the same step in replica mode (every rank its own set, no collective)
+            rseed = harness.rank_seed(synth.BASE_SEED, rank, args.config)
+            rnames, rseqs = synth.genome_set(args.config, seed=rseed)
+            rcomm = None
+        else:        # one set (rank 0's seed) sharded over the ranks on the communicator
+            rnames, rseqs = synth.genome_set(args.config, seed=harness.rank_seed(synth.BASE_SEED, 0, args.config))
+            rcomm = comm
+        rss = _capi.SeqSet(rseqs, rnames)
+        rjob = pipeline.BlockBuild(rss, rnames, rseqs, comm=rcomm, anchor_loop=args.anchor_loop)
+        rdt, _ = harness.timed_steps(rjob.run, args.steps, args.warmup, dist,
+                                     sync=torch.cuda.synchronize, device="cuda")
+        rbp = synth.total_bp(rseqs)
+        other = {"value": round(harness.throughput(rbp, world if sharded else 1, args.steps, rdt) / 1e6, 3),
+                 "unit": "Mbp/s", "ms_per_step": round(rdt / args.steps * 1e3, 4),
+                 "scaling": "weak" if sharded else "strong",
+                 "parallelism": ("replica-per-gpu x%d (independent sets, no collective)" % world) if sharded
+                 else "sharded x%d (one set: AnchorFinder windows and aligner jobs over the ranks; %s)"
+                      % (world, "library RCCL communicator" if args.dist_backend == "nccl" else args.dist_backend)}
+        del rjob, rss
+    pairs_line = None
+    if not args.no_pairs_line and args.anchor_loop is False:
+        # BASELINE C4's split at every N: genome pairs over the ranks, RCCL gather at the end
+        pairs_line = run_pairs(args, dist, world, rank, local_rank, comm, args.pairs_config, args.pairs,
+                               min(args.steps, 2), 1, baseline=False)
+        if pairs_line is not None:
+            pairs_line = {k: pairs_line[k] for k in ("value", "unit", "ms_per_step", "scaling", "config",
+                                                     "last_step", "device_mem_used_gb", "roofline")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -182,54 +210,55 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded Brucella-like proxy, npge_amd/synth.py)",
-            "config": {"workload": job.workload_name(args.config), "bp_per_rank": bp,
+            "config": {"workload": workload, "bp_per_rank": bp,
                        "genomes": synth.CONFIGS[args.config][0], "anchor_size": 20,
                        "anchor_fp": 0.1, "max_anchor_fragments": 100000,
                        "inputs": "resident in HBM before the timed region (upload: pcie_inclusive)",
                        "parallelism": ("sharded x%d (one set; %s)" % (world, "library RCCL communicator"
                                                                        if args.dist_backend == "nccl" else
                                                                        args.dist_backend)) if sharded
-                       else "replica-per-gpu x%d" % world},
+                       else "replica-per-gpu x%d (independent sets, no data-path collective)" % world},
             "last_step": info,
             "kernels_last_step": kernels,
             "roofline": roofline,
             "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
-            "replicas": replicas,
+            ("replicas" if sharded else "sharded"): other,
+            "pairs": pairs_line,
         }
         print(json.dumps(line), flush=True)
+    finish(dist, world, comm)
+
+
+def finish(dist, world, comm):
+    import gc
+    gc.collect()  # block sets hold the communicator: free them first
     if world > 1:
         if comm is not None and hasattr(comm, "close"):
-            del job
             comm.close()
         dist.destroy_process_group()
 
 
-def main_pairs(args, dist, world, rank, local_rank):
-    """--mode pairs: the pair-sharded job (npge_amd/pairs.py).  One step = every
-    pair of the set through DraftPangenome once (the rank's share, --pair-workers
-    at a time) + the final all-gather of every pair's blocks."""
+def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps, warmup, baseline):
+    """The pair-sharded job (npge_amd/pairs.py, BASELINE C4's split).  One step =
+    every pair of the set through DraftPangenome once (the rank's share,
+    --pair-workers at a time) + the final all-gather of every pair's blocks
+    over `comm`.  Returns rank 0's line (None on other ranks)."""
+    import gc
     import torch
-    from npge_amd import comm as ncomm, harness, pairs, synth
-    names, seqs = synth.genome_set(args.config)
+    from npge_amd import harness, pairs, synth
+    names, seqs = synth.genome_set(config)
     sel = pairs.all_pairs(names)
-    if args.pairs:
-        sel = sel[:args.pairs]
-    comm = None
-    if world > 1:
-        if args.dist_backend == "nccl":
-            comm = ncomm.RcclComm(dist, local_rank)
-        else:
-            comm = ncomm.TorchComm(dist, staging="cpu")
-        ncomm.check(comm)
+    if n_pairs:
+        sel = sel[:n_pairs]
     gdev = torch.device("cuda", local_rank) if world > 1 and args.dist_backend == "nccl" else None
     job = pairs.PairJobs(names, seqs, rank=rank, world=world, comm=comm, workers=args.pair_workers,
                          pairs=sel, device=local_rank, gather_device=gdev)
     torch.cuda.synchronize()
-    dt, info = harness.timed_steps(job.run, args.steps, args.warmup, dist if world > 1 else None,
+    dt, info = harness.timed_steps(job.run, steps, warmup, dist if world > 1 else None,
                                    sync=torch.cuda.synchronize, device="cuda")
     total = job.total_bp()
-    value = total * args.steps / dt / 1e6          # the whole pair job over the max-over-ranks time
+    value = total * steps / dt / 1e6          # the whole pair job over the max-over-ranks time
     agg = {}
     for _, _, bb in job.jobs:
         for k in bb.kernel_times():
@@ -237,6 +266,9 @@ def main_pairs(args, dist, world, rank, local_rank):
             a["ms"] += k["ms"]
             a["bytes"] += k["bytes"]
             a["launches"] += k["launches"]
+    mem = round((lambda f: (f[1] - f[0]) / 2**30)(torch.cuda.mem_get_info()), 2)
+    del job
+    gc.collect()
     kern = [k for k in agg.values() if not k["name"].endswith("_allreduce")]
     dom = max(kern, key=lambda k: k["ms"]) if kern else None
     roofline = None
@@ -247,38 +279,34 @@ def main_pairs(args, dist, world, rank, local_rank):
                     "launches_per_rank_step": dom["launches"],
                     "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                     "bytes_per_launch": dom["bytes"] / dom["launches"],
-                    "note": "kernel times summed over the rank's pairs (concurrent streams overlap)"}
+                    "note": "HIP-event kernel times summed over the rank's pairs; concurrent pairs' "
+                            "events overlap, so this understates the kernel's rate"}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and baseline:
         cpu = cpu_baseline_pair(names, seqs, sel[0], args.cpu_runs)
-    if rank == 0:
-        line = {
-            "metric": "anchored+aligned Mbp/sec at 1/2/4/8 MI355X; bit-exact anchor set vs CPU",
-            "value": round(value, 3), "unit": "Mbp/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded, npge_amd/synth.py)",
-            "config": {"workload": "%s pair-sharded: DraftPangenome per genome pair (%d pairs, %d bp), "
-                                   "final all-gather of every pair's blocks" % (args.config, len(sel), total),
-                       "genomes": synth.CONFIGS[args.config][0], "pairs": len(sel), "bp_job": total,
-                       "pair_workers": args.pair_workers,
-                       "inputs": "every pair's sequences resident in HBM before the timed region",
-                       "parallelism": "pairs round-robin over %d rank(s); %s" % (
-                           world, "library RCCL communicator" if comm is not None and args.dist_backend == "nccl"
-                           else (args.dist_backend if world > 1 else "no collective"))},
-            "last_step": info,
-            "device_mem_used_gb": round((lambda f: (f[1] - f[0]) / 2**30)(torch.cuda.mem_get_info()), 2),
-            "kernels_last_step": sorted(({"name": k["name"], "ms": round(k["ms"], 4), "launches": k["launches"]}
-                                         for k in agg.values()), key=lambda k: -k["ms"])[:12],
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        del job
-        if comm is not None and hasattr(comm, "close"):
-            comm.close()
-        dist.destroy_process_group()
+    if rank != 0:
+        return None
+    return {
+        "metric": "anchored+aligned Mbp/sec at 1/2/4/8 MI355X; bit-exact anchor set vs CPU",
+        "value": round(value, 3), "unit": "Mbp/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded, npge_amd/synth.py)",
+        "config": {"workload": "%s pair-sharded: DraftPangenome per genome pair (%d pairs, %d bp), "
+                               "final all-gather of every pair's blocks" % (config, len(sel), total),
+                   "genomes": synth.CONFIGS[config][0], "pairs": len(sel), "bp_job": total,
+                   "pair_workers": args.pair_workers,
+                   "inputs": "every pair's sequences resident in HBM before the timed region",
+                   "parallelism": "pairs round-robin over %d rank(s); %s" % (
+                       world, "library RCCL communicator" if comm is not None and args.dist_backend == "nccl"
+                       else (args.dist_backend if world > 1 else "no collective"))},
+        "last_step": info,
+        "device_mem_used_gb": mem,
+        "kernels_last_step": sorted(({"name": k["name"], "ms": round(k["ms"], 4), "launches": k["launches"]}
+                                     for k in agg.values()), key=lambda k: -k["ms"])[:12],
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
 
 
 def cpu_baseline_pair(names, seqs, idx, runs):

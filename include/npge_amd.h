@@ -330,6 +330,13 @@ typedef struct {
 
 void npgx_bb_default_options(npgx_bb_options* o);
 int npgx_blockset_create(const npgx_seqset* s, const npgx_bb_options* o, npgx_blockset** out);
+/* as npgx_blockset_create, but the new set borrows lender's aligner (its device
+ * scratch and HIP stream) instead of making one: the two sets must not run at
+ * the same time (one host thread), and lender must outlive the new set.  The
+ * pair-sharded job (npge_amd/pairs.py) runs its pairs this way, one lender per
+ * worker thread.  No reference counterpart: a device-memory sharing hint. */
+int npgx_blockset_create_sharing(const npgx_seqset* s, const npgx_bb_options* o, npgx_blockset* lender,
+                                 npgx_blockset** out);
 /* replace the blocks; row_off == NULL: no rows, else row i = rows[row_off[i]..row_off[i+1])
  * (a block whose rows are all empty is unaligned) */
 int npgx_blockset_set_blocks(npgx_blockset* b, int64_t n_blocks, const int64_t* block_start,

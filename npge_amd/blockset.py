@@ -53,6 +53,7 @@ def _bind(L):
     L.npgx_bb_default_options.argtypes = [P(BbOptions)]
     L.npgx_bb_default_options.restype = None
     L.npgx_blockset_create.argtypes = [vp, P(BbOptions), P(vp)]
+    L.npgx_blockset_create_sharing.argtypes = [vp, P(BbOptions), vp, P(vp)]
     L.npgx_blockset_set_blocks.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp]
     L.npgx_blockset_add_anchors.argtypes = [vp, vp]
     L.npgx_blockset_set_comm.argtypes = [vp, vp]
@@ -92,12 +93,19 @@ def default_options(**kw):
 class BlockSetEngine:
     """One npgx_blockset over a device sequence set."""
 
-    def __init__(self, seqset, options=None, **kw):
+    def __init__(self, seqset, options=None, lender=None, **kw):
+        """lender: another engine whose aligner this one borrows
+        (npgx_blockset_create_sharing): never run the two at the same time."""
         L = _bind(_capi.lib())
         self.ss = seqset
         o = options or default_options(**kw)
         h = ctypes.c_void_p()
-        _capi.check(L.npgx_blockset_create(seqset.handle, ctypes.byref(o), ctypes.byref(h)))
+        if lender is None:
+            _capi.check(L.npgx_blockset_create(seqset.handle, ctypes.byref(o), ctypes.byref(h)))
+        else:
+            _capi.check(L.npgx_blockset_create_sharing(seqset.handle, ctypes.byref(o), lender._h,
+                                                       ctypes.byref(h)))
+        self._lender = lender  # freed after this engine
         self._h = h
 
     def set_comm(self, comm):

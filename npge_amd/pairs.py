@@ -8,9 +8,11 @@ sequences -- the same call the reference's `npge` runs on a two-genome input,
 so each pair's blocks are bit-exact with the CPU path on that pair
 (tests/test_pairs_gpu.py against oracle/).  Pairs go to ranks round-robin in
 pair order (all pairs of a config have about the same size); on its GPU a
-rank runs `workers` pairs at a time, each on its own host thread with its own
-sequence set, block set, aligner and AnchorFinder handle (one HIP stream
-each), so that the latency-bound iterations of one pair overlap the others'.
+rank runs `workers` pairs at a time, each worker on its own host thread with
+its own aligner (device scratch and HIP stream), which the block sets of the
+worker's pairs borrow in turn (npgx_blockset_create_sharing); every pair has
+its own sequence set, block set and AnchorFinder handle.  The latency-bound
+iterations of one pair overlap the other workers' pairs.
 The data path has no collective until the end: every rank's anchored+aligned
 blocks -- fragment coordinates per pair -- are all-gathered once over the
 communicator (RCCL over xGMI on the GPU box: the library's own npgx_comm), so
@@ -137,12 +139,16 @@ class PairJobs:
         self.device = device
         self.gather_device = gather_device
         self.pair_bp = [sum(len(seqs[i]) for i in self.pairs[p]) for p in range(len(self.pairs))]
+        # worker w runs the rank's pairs w, w + workers, ... one after another,
+        # all on the aligner of its first pair (npgx_blockset_create_sharing):
+        # device memory is one aligner's scratch per worker, not per pair
         self.jobs = []
-        for p in self.mine:
+        for k, p in enumerate(self.mine):
             idx = self.pairs[p]
             pn, ps = [names[i] for i in idx], [seqs[i] for i in idx]
             ss = _capi.SeqSet(ps, pn)
-            self.jobs.append((p, ss, BlockBuild(ss, pn, ps)))
+            lender = self.jobs[k % self.workers][2] if k >= self.workers else None
+            self.jobs.append((p, ss, BlockBuild(ss, pn, ps, lender=lender)))
         self.records = None
         self.summary = None
 
@@ -155,18 +161,14 @@ class PairJobs:
 
     def _run_pairs(self):
         from . import _capi
-        nxt = iter(range(len(self.jobs)))
-        lock = threading.Lock()
         infos = [None] * len(self.jobs)
         errors = []
 
-        def worker():
+        def worker(w):
             try:
                 _capi.check(_capi.lib().npgx_set_device(self.device))
-                while True:
-                    with lock:
-                        k = next(nxt, None)
-                    if k is None or errors:
+                for k in range(w, len(self.jobs), self.workers):
+                    if errors:
                         return
                     infos[k] = self.jobs[k][2].run()
             except Exception as e:  # re-raised on the calling thread
@@ -174,9 +176,9 @@ class PairJobs:
 
         n = min(self.workers, len(self.jobs))
         if n <= 1:
-            worker()
+            worker(0)
         else:
-            ts = [threading.Thread(target=worker) for _ in range(n)]
+            ts = [threading.Thread(target=worker, args=(w,)) for w in range(n)]
             for t in ts:
                 t.start()
             for t in ts:

@@ -12,15 +12,18 @@ STAGES = ["AnchorFinder", "RemoveNonStem", "DummyAligner", "ExtendLoopFast(10)",
 
 
 class BlockBuild:
-    def __init__(self, seqset, names, seqs, seed=1, comm=None, anchor_loop=False):
+    def __init__(self, seqset, names, seqs, seed=1, comm=None, anchor_loop=False, lender=None):
         self.ss = seqset
         self.seed = seed
         self.anchor_loop = anchor_loop
         self.loop_af = AnchorFinder() if anchor_loop else None
-        self.eng = BlockSetEngine(seqset)
+        # lender: a BlockBuild whose aligner this one borrows (never run together)
+        self.eng = BlockSetEngine(seqset, lender=lender.eng if lender is not None else None)
         if comm is not None:  # one genome set sharded over the ranks of comm
             self.eng.set_comm(comm)
-        self.af = AnchorFinder()
+        # the AnchorFinder handle: its own, or the lender's (its window layout is
+        # rebuilt when the sequence set changes, its used set cleared per run)
+        self.af = lender.af if lender is not None else AnchorFinder()
         self.af.set_opt_value("bloom-seed", self.seed)
 
     def workload_name(self, config):

@@ -1,7 +1,8 @@
 """bench.py's multi-rank paths on the GPU box's one GPU: two ranks launched by
 torch.distributed.run with the gloo backend (rehearsal of the driver's RCCL
-runs; ranks share the GPU), replicas and sharded modes.  Checks the JSON
-contract fields and that the sharded line reports one set's bp."""
+runs; ranks share the GPU), replicas, sharded and pairs modes.  Checks the
+JSON contract fields, that the sharded line reports one set's bp, and the
+secondary lines (one set sharded / replicas, the pair-sharded job)."""
 import json
 import os
 import socket
@@ -22,12 +23,12 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("mode", ["replicas", "sharded"])
+@pytest.mark.parametrize("mode", ["replicas", "sharded", "pairs"])
 def test_bench_two_ranks_gloo(mode):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
            "--steps", "1", "--warmup", "1", "--config", "small", "--mode", mode,
-           "--dist-backend", "gloo", "--no-cpu-baseline"]
+           "--dist-backend", "gloo", "--no-cpu-baseline", "--pairs-config", "small", "--pair-workers", "2"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -37,9 +38,17 @@ def test_bench_two_ranks_gloo(mode):
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
     assert d["n_gpus"] == 2 and d["value"] > 0
+    if mode == "pairs":  # 10 pairs of the 5-genome set over 2 ranks, all gathered on rank 0
+        assert d["scaling"] == "strong" and d["config"]["pairs"] == 10
+        assert d["last_step"]["gathered_pairs"] == 10 and d["last_step"]["pairs_rank"] == 5
+        assert abs(d["value"] - d["config"]["bp_job"] / (d["ms_per_step"] / 1e3) / 1e6) / d["value"] < 1e-3
+        return
+    assert d["pairs"]["value"] > 0 and d["pairs"]["last_step"]["gathered_pairs"] == 10
     bp = d["config"]["bp_per_rank"]
     ranks = 1 if mode == "sharded" else 2
     assert abs(d["value"] - bp * ranks / (d["ms_per_step"] / 1e3) / 1e6) / d["value"] < 1e-3
     assert d["scaling"] == ("strong" if mode == "sharded" else "weak")
     if mode == "sharded":  # the secondary replica-mode measurement of the same step
         assert d["replicas"]["value"] > 0 and d["replicas"]["scaling"] == "weak"
+    else:                  # the secondary one-set sharded measurement
+        assert d["sharded"]["value"] > 0 and d["sharded"]["scaling"] == "strong"

@@ -58,3 +58,30 @@ def test_torch_comm_check_gloo_two_ranks():
         print("ok")
     ''', world=2)
     assert all(o.strip().endswith("ok") for o in out)
+
+
+def test_rccl_world_one_pair_gather():
+    """The pair-sharded job's final gather through the library's RCCL
+    communicator with device exchange buffers (the driver's N > 1 path):
+    at world size 1 the gathered records equal the rank's own."""
+    out = _run('''
+        import sys
+        sys.path.insert(0, ".")
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        from npge_amd import _capi, comm, pairs, synth
+        _capi.check(_capi.lib().npgx_set_device(0))
+        c = comm.RcclComm(dist, 0)
+        names, seqs = synth.genome_set("tiny")
+        job = pairs.PairJobs(names, seqs, comm=c, workers=2, gather_device=torch.device("cuda", 0))
+        info = job.run()
+        frs, sums = job.local_records()
+        assert info["gathered_pairs"] == 3 and len(frs) > 0
+        assert np.array_equal(job.records, frs) and np.array_equal(job.summary, sums)
+        del job
+        c.close()
+        print("ok")
+    ''')
+    assert out[0].strip().endswith("ok")

@@ -162,6 +162,7 @@ class PairJobs:
     def _run_pairs(self):
         from . import _capi
         infos = [None] * len(self.jobs)
+        recs = self._recs = [None] * len(self.jobs)
         errors = []
 
         def worker(w):
@@ -171,6 +172,7 @@ class PairJobs:
                     if errors:
                         return
                     infos[k] = self.jobs[k][2].run()
+                    recs[k] = self._records(k)  # packed on the worker, overlapping the others' pairs
             except Exception as e:  # re-raised on the calling thread
                 errors.append(e)
 
@@ -187,20 +189,27 @@ class PairJobs:
             raise errors[0]
         return infos
 
+    def _records(self, k):
+        """(fragment records, summary record) of the rank's k-th pair."""
+        p, _, job = self.jobs[k]
+        bs, seq, mn, mx, ori = job.eng.fragments()
+        return (pack_fragments(p, bs, seq, mn, mx, ori),
+                np.array([(p << 32) | (len(bs) - 1), job.eng.hash()], dtype=np.uint64))
+
     def local_records(self):
-        frs, sums = [], []
-        for p, _, job in self.jobs:
-            bs, seq, mn, mx, ori = job.eng.fragments()
-            frs.append(pack_fragments(p, bs, seq, mn, mx, ori))
-            sums.append(np.array([(p << 32) | (len(bs) - 1), job.eng.hash()], dtype=np.uint64))
+        recs = [self._records(k) for k in range(len(self.jobs))]
+        return self._cat(recs)
+
+    @staticmethod
+    def _cat(recs):
         cat = (lambda a: np.concatenate(a) if a else np.zeros(0, dtype=np.uint64))
-        return cat(frs), cat(sums)
+        return cat([r[0] for r in recs]), cat([r[1] for r in recs])
 
     def run(self):
         t0 = time.perf_counter()
         infos = self._run_pairs()
         t1 = time.perf_counter()
-        frs, sums = self.local_records()
+        frs, sums = self._cat(self._recs)
         if self.comm is not None:  # the one collective: the final anchored-block gather
             frs, _ = gather_u64(self.comm, frs, self.gather_device)
             sums, _ = gather_u64(self.comm, sums, self.gather_device)
@@ -212,7 +221,12 @@ class PairJobs:
                 "gathered_fragments": int(len(frs) // 2), "gathered_pairs": int(len(sums) // 2),
                 "stem_blocks": int(sum(i["stem_blocks"] for i in done)),
                 "aligned_residues": int(sum(i["aligned_residues"] for i in done)),
-                "align_jobs": int(sum(i["align_jobs"] for i in done))}
+                "align_jobs": int(sum(i["align_jobs"] for i in done)),
+                # one pair's engine timings, averaged (wall clock of its own thread)
+                "mean_pair_ms": {k: round(sum(i["ms_stage"][k] for i in done) / max(len(done), 1), 3)
+                                 for k in (done[0]["ms_stage"] if done else {})},
+                "mean_pair_ms_align": round(sum(i["ms_align_wall"] for i in done) / max(len(done), 1), 3),
+                "mean_pair_ms_host": round(sum(i["ms_host_bookkeeping"] for i in done) / max(len(done), 1), 3)}
 
     def hashes(self):
         """{pair: blockset hash} of the gathered summaries (after run())."""

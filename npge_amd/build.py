@@ -28,8 +28,8 @@ def _stale(lib=LIB):
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False, profile=False):
-    lib = LIB_PROF if profile else LIB
+def build(force=False, verbose=False, profile=False, lib_path=None):
+    lib = lib_path or (LIB_PROF if profile else LIB)
     if not force and not _stale(lib):
         return lib
     objs = []

@@ -27,22 +27,22 @@ if [ "$PART" = tests ]; then
 else
   for cfg in C2 C4 C5; do
     step bench_$cfg
-    timeout -k 10 300 python bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_$cfg.log 2>&1 || { tail -5 $O/bench_$cfg.log; exit 1; }
+    timeout -k 10 300 python bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/bench_$cfg.log 2>&1 || { tail -5 $O/bench_$cfg.log; exit 1; }
     tail -1 $O/bench_$cfg.log | cut -c1-200
   done
   for cfg in C3 C4; do
     step bench_${cfg}_alf
-    timeout -k 10 300 python bench.py --config $cfg --anchor-loop --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_${cfg}_alf.log 2>&1 || { tail -5 $O/bench_${cfg}_alf.log; exit 1; }
+    timeout -k 10 300 python bench.py --config $cfg --anchor-loop --steps 3 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/bench_${cfg}_alf.log 2>&1 || { tail -5 $O/bench_${cfg}_alf.log; exit 1; }
     tail -1 $O/bench_${cfg}_alf.log | cut -c1-200
   done
   step bench_dp
   timeout -k 10 300 python tools/bench_dp.py > $O/bench_dp.log 2>&1 || { tail -5 $O/bench_dp.log; exit 1; }
   step rocprof_c3
   cd /tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_c3.log 2>&1 || { tail -5 $O/prof_c3.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/prof_c3.log 2>&1 || { tail -5 $O/prof_c3.log; exit 1; }
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_$c
-    timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/c3_$c -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_$c.log 2>&1 || { tail -5 $O/pmc_$c.log; exit 1; }
+    timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/c3_$c -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/pmc_$c.log 2>&1 || { tail -5 $O/pmc_$c.log; exit 1; }
   done
 fi
 step done

@@ -17,7 +17,13 @@ from npge_amd.blockset import BlockSetEngine
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
 _capi.check(_capi.lib().npgx_set_device(0))
-names, seqs = synth.genome_set(cfg)
+if cfg.endswith(":pair"):  # the first genome pair of a config (the pair-sharded job's unit)
+    from npge_amd import pairs as _pairs
+    names, seqs = synth.genome_set(cfg.split(":")[0])
+    idx = _pairs.all_pairs(names)[0]
+    names, seqs = [names[i] for i in idx], [seqs[i] for i in idx]
+else:
+    names, seqs = synth.genome_set(cfg)
 ss = _capi.SeqSet(seqs, names)
 eng = BlockSetEngine(ss)
 best = None

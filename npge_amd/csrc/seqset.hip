@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <memory>
 #include <numeric>
 
@@ -138,9 +139,24 @@ void heavy_for(size_t n, int64_t work, const std::function<void(size_t)>& f) {
     if (err) std::rethrow_exception(err);
 }
 
+// Poll the stream (a blocking hipStreamSynchronize costs tens of us of wake-up
+// on every short wait of the block build).  When several host threads wait at
+// once (the pair-sharded job runs a dozen block sets on one GPU) a waiter
+// that has polled for a while sleeps between polls instead: a dozen threads
+// spinning on hipStreamQuery took the runtime's locks and the host cores from
+// the threads with work to do.
 hipError_t stream_wait(hipStream_t s) {
+    static std::atomic<int> waiters{0};
+    waiters.fetch_add(1, std::memory_order_relaxed);
     hipError_t e;
-    while ((e = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
+    int polls = 0;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+        if (++polls > 64 && waiters.load(std::memory_order_relaxed) > 1)
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else
+            __builtin_ia32_pause();
+    }
+    waiters.fetch_sub(1, std::memory_order_relaxed);
     return e;
 }
 

@@ -206,9 +206,14 @@ class PairJobs:
         return cat([r[0] for r in recs]), cat([r[1] for r in recs])
 
     def run(self):
+        import resource
+        r0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         infos = self._run_pairs()
         t1 = time.perf_counter()
+        r1 = resource.getrusage(resource.RUSAGE_SELF)
+        # host cores kept busy while the pairs ran (user + system CPU time / wall)
+        cores_busy = ((r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)) / max(t1 - t0, 1e-9)
         frs, sums = self._cat(self._recs)
         if self.comm is not None:  # the one collective: the final anchored-block gather
             frs, _ = gather_u64(self.comm, frs, self.gather_device)
@@ -218,6 +223,7 @@ class PairJobs:
         done = [i for i in infos if i is not None]
         return {"pairs": len(self.pairs), "pairs_rank": len(self.jobs), "workers": self.workers,
                 "ms_pairs": round((t1 - t0) * 1e3, 3), "ms_gather": round((t2 - t1) * 1e3, 3),
+                "host_cores_busy": round(cores_busy, 2),
                 "gathered_fragments": int(len(frs) // 2), "gathered_pairs": int(len(sums) // 2),
                 "stem_blocks": int(sum(i["stem_blocks"] for i in done)),
                 "aligned_residues": int(sum(i["aligned_residues"] for i in done)),

@@ -339,7 +339,9 @@ def pmc_traffic(kernel, config):
     tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
     of this bench).  PMC counters cannot be read from inside this process."""
     import glob
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_%s_pmc_traffic.json" % config.lower())))
+    # newest session tag: r03z < r03aa < r03ab (shorter tags first)
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_%s_pmc_traffic.json" % config.lower())),
+                   key=lambda f: (len(os.path.basename(f).split("_")[0]), os.path.basename(f)))
     if not files:
         return {"traffic": None}
     doc = json.load(open(files[-1]))

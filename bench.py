@@ -185,10 +185,11 @@ def main():
     if not args.no_pairs_line and args.anchor_loop is False:
         # BASELINE C4's split at every N: genome pairs over the ranks, RCCL gather at the end
         pairs_line = run_pairs(args, dist, world, rank, local_rank, comm, args.pairs_config, args.pairs,
-                               min(args.steps, 2), 1, baseline=False)
+                               min(args.steps, 2), 1, baseline=not args.no_cpu_baseline, cpu_runs=1)
         if pairs_line is not None:
             pairs_line = {k: pairs_line[k] for k in ("value", "unit", "ms_per_step", "scaling", "config",
-                                                     "last_step", "device_mem_used_gb", "roofline")}
+                                                     "last_step", "device_mem_used_gb", "roofline",
+                                                     "cpu_baseline")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -239,7 +240,7 @@ def finish(dist, world, comm):
         dist.destroy_process_group()
 
 
-def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps, warmup, baseline):
+def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps, warmup, baseline, cpu_runs=None):
     """The pair-sharded job (npge_amd/pairs.py, BASELINE C4's split).  One step =
     every pair of the set through DraftPangenome once (the rank's share,
     --pair-workers at a time) + the final all-gather of every pair's blocks
@@ -283,7 +284,7 @@ def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps,
                             "events overlap, so this understates the kernel's rate"}
     cpu = None
     if rank == 0 and world == 1 and baseline:
-        cpu = cpu_baseline_pair(names, seqs, sel[0], args.cpu_runs)
+        cpu = cpu_baseline_pair(names, seqs, sel[0], cpu_runs or args.cpu_runs)
     if rank != 0:
         return None
     return {

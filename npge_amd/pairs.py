@@ -30,9 +30,9 @@ import time
 import numpy as np
 
 # record layout of one fragment (2 x u64):
-#   w0 = pair << 44 | block << 4 | local_seq << 1 | (ori > 0)
+#   w0 = pair << 44 | block << 12 | local_seq << 1 | (ori > 0)
 #   w1 = min << 32 | max
-PAIR_BITS, BLOCK_BITS, SEQ_BITS = 20, 40, 3
+PAIR_BITS, BLOCK_BITS, SEQ_BITS = 20, 32, 11
 # per-pair summary record (2 x u64): (pair << 32 | n_blocks), blockset hash
 
 
@@ -65,7 +65,7 @@ def pack_fragments(pair, bs, seq, mn, mx, ori):
     assert pair < (1 << PAIR_BITS) and nb < (1 << BLOCK_BITS)
     assert int(seq[:nf].max()) < (1 << SEQ_BITS) and int(mx[:nf].max()) < (1 << 32)
     blk = np.repeat(np.arange(nb, dtype=np.uint64), np.diff(bs).astype(np.int64))
-    w0 = ((np.uint64(pair) << np.uint64(44)) | (blk << np.uint64(4))
+    w0 = ((np.uint64(pair) << np.uint64(44)) | (blk << np.uint64(12))
           | (seq[:nf].astype(np.uint64) << np.uint64(1)) | (ori[:nf] > 0).astype(np.uint64))
     w1 = (mn[:nf].astype(np.uint64) << np.uint64(32)) | mx[:nf].astype(np.uint64)
     return np.stack([w0, w1], axis=1).reshape(-1)
@@ -76,11 +76,11 @@ def unpack_fragments(rec):
     r = rec.reshape(-1, 2)
     out = {}
     for w0, w1 in r.tolist():
-        p, b = w0 >> 44, (w0 >> 4) & ((1 << BLOCK_BITS) - 1)
+        p, b = w0 >> 44, (w0 >> 12) & ((1 << BLOCK_BITS) - 1)
         blocks = out.setdefault(p, [])
         while len(blocks) <= b:
             blocks.append([])
-        blocks[b].append(((w0 >> 1) & 7, w1 >> 32, w1 & 0xffffffff, 1 if w0 & 1 else -1))
+        blocks[b].append(((w0 >> 1) & ((1 << SEQ_BITS) - 1), w1 >> 32, w1 & 0xffffffff, 1 if w0 & 1 else -1))
     return out
 
 

@@ -51,7 +51,7 @@ def _blocks(rng, nb, nseq):
 
 def test_record_round_trip():
     rng = np.random.default_rng(3)
-    bs, seq, mn, mx, ori = _blocks(rng, 300, 4)
+    bs, seq, mn, mx, ori = _blocks(rng, 300, 2047)   # up to 2047 sequences in a pair
     rec = pairs.pack_fragments(495, bs, seq, mn, mx, ori)
     assert rec.dtype == np.uint64 and len(rec) == 2 * int(bs[-1])
     got = pairs.unpack_fragments(rec)[495]

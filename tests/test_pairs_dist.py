@@ -91,3 +91,14 @@ def test_gather_over_gloo(world):
         assert len(got) == sum(counts)
         assert np.array_equal(got, out[0][0])
         assert pairs.unpack_fragments(got) == want
+
+
+def test_pair_cpu_baseline_record():
+    """bench.py's CPU leg for the pair job: the oracle's DraftPangenome on one
+    pair, timed (no GPU); the record names its sample and cores."""
+    import bench
+    names, seqs = synth.genome_set("tiny")
+    idx = pairs.all_pairs(names)[0]
+    r = bench.cpu_baseline_pair(names, seqs, idx, 1)
+    assert r["value"] > 0 and r["cores"] == 1 and r["kind"] == "port"
+    assert "G01" in r["sample"] and "G02" in r["sample"] and r["workload"] == "DraftPangenome"

@@ -62,17 +62,80 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default=None, help="synthetic config timed for cpu_baseline (default: --config)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU runs (median) after one warm-up")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only the rank launch and rendezvous (no GPU call): prints n_gpus and the "
+                         "communicator's rank count (tests/test_bench_launch.py)")
     a = ap.parse_args()
     if a.config is None:
         a.config = "C4" if a.mode == "pairs" else "C3"
     return a
 
 
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher (no WORLD_SIZE in the environment):
+    start the N ranks as child processes of torch.distributed.run, one per GPU,
+    before this process makes any GPU call, and return their exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, NPGX_BENCH_LAUNCHER="bench.py")
+    return subprocess.call(cmd, env=env)
+
+
+def ranks_from_env(args):
+    """(world, rank, local_rank) of this process; --gpus N must equal the
+    launcher's WORLD_SIZE (a mismatch exits non-zero)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d: every GPU is one rank, refusing to run"
+              % (args.gpus, world), file=sys.stderr, flush=True)
+        sys.exit(2)
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def launcher_name():
+    if os.environ.get("NPGX_BENCH_LAUNCHER"):
+        return "bench.py -> torch.distributed.run"
+    return "external (torch.distributed.run)" if "WORLD_SIZE" in os.environ else "none (one process)"
+
+
+def launch_check(args, world, rank):
+    """The rendezvous alone, with no GPU call: every rank joins the process
+    group, the npgx_comm binding (host staging) all-gathers every rank's id,
+    and rank 0 prints the rank counts."""
+    import ctypes
+    import torch.distributed as dist
+    from npge_amd import pairs
+    from npge_amd.comm import TorchComm
+    if world > 1:
+        dist.init_process_group(args.dist_backend)
+        comm = TorchComm(dist, staging="cpu", copy=ctypes.memmove)
+        import numpy as np
+        ids, counts = pairs.gather_u64(comm, np.array([rank], dtype=np.uint64))
+        assert ids.tolist() == list(range(world)) and counts == [1] * world
+        comm_ranks = comm.world
+    else:
+        comm_ranks = 1
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "comm_ranks": comm_ranks,
+                          "launcher": launcher_name(), "dist_backend": args.dist_backend}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))  # nothing here has touched the GPU
+    world, rank, local_rank = ranks_from_env(args)
+    if args.launch_check:
+        launch_check(args, world, rank)
+        return
 
     import torch
     import torch.distributed as dist
@@ -97,10 +160,15 @@ def main():
         else:  # gloo rehearsal: ranks may share a GPU (RCCL refuses that)
             comm = ncomm.TorchComm(dist, staging="cpu")
         ncomm.check(comm)  # every collective once, results verified, before any timing
+        if comm.count() != world:
+            raise SystemExit("bench.py: the communicator has %d ranks, WORLD_SIZE is %d" % (comm.count(), world))
+    comm_ranks = comm.count() if comm is not None else 1
     if args.mode == "pairs":
         line = run_pairs(args, dist, world, rank, local_rank, comm, args.config, args.pairs,
                          args.steps, args.warmup, baseline=not args.no_cpu_baseline)
         if rank == 0:
+            line["comm_ranks"] = comm_ranks
+            line["launcher"] = launcher_name()
             print(json.dumps(line), flush=True)
         finish(dist, world, comm)
         return
@@ -185,7 +253,7 @@ def main():
     if not args.no_pairs_line and args.anchor_loop is False:
         # BASELINE C4's split at every N: genome pairs over the ranks, RCCL gather at the end
         pairs_line = run_pairs(args, dist, world, rank, local_rank, comm, args.pairs_config, args.pairs,
-                               min(args.steps, 2), 1, baseline=not args.no_cpu_baseline, cpu_runs=1)
+                               min(args.steps, 2), 1, baseline=not args.no_cpu_baseline, cpu_runs=3)
         if pairs_line is not None:
             pairs_line = {k: pairs_line[k] for k in ("value", "unit", "ms_per_step", "scaling", "config",
                                                      "last_step", "device_mem_used_gb", "roofline",
@@ -203,6 +271,8 @@ def main():
             "value": round(value, 3),
             "unit": "Mbp/s",
             "n_gpus": world,
+            "comm_ranks": comm_ranks,
+            "launcher": launcher_name(),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
@@ -260,13 +330,8 @@ def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps,
                                    sync=torch.cuda.synchronize, device="cuda")
     total = job.total_bp()
     value = total * steps / dt / 1e6          # the whole pair job over the max-over-ranks time
-    agg = {}
-    for _, _, bb in job.jobs:
-        for k in bb.kernel_times():
-            a = agg.setdefault(k["name"], {"name": k["name"], "ms": 0.0, "bytes": 0.0, "launches": 0})
-            a["ms"] += k["ms"]
-            a["bytes"] += k["bytes"]
-            a["launches"] += k["launches"]
+    set_bp = synth.total_bp(seqs)             # the genome set itself (each genome is in G - 1 pairs)
+    agg = {k["name"]: k for k in job.kernel_times()}  # each pair's own times, taken right after it ran
     mem = round((lambda f: (f[1] - f[0]) / 2**30)(torch.cuda.mem_get_info()), 2)
     del job
     gc.collect()
@@ -280,16 +345,21 @@ def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps,
                     "launches_per_rank_step": dom["launches"],
                     "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                     "bytes_per_launch": dom["bytes"] / dom["launches"],
-                    "note": "HIP-event kernel times summed over the rank's pairs; concurrent pairs' "
-                            "events overlap, so this understates the kernel's rate"}
+                    "note": "HIP-event kernel times of every pair of the rank, each pair's collected on its "
+                            "worker right after it ran; concurrent pairs' events overlap, so this understates "
+                            "the kernel's rate"}
     cpu = None
     if rank == 0 and world == 1 and baseline:
-        cpu = cpu_baseline_pair(names, seqs, sel[0], cpu_runs or args.cpu_runs)
+        cpu = cpu_baseline_pair(names, seqs, sel, cpu_runs or args.cpu_runs)
     if rank != 0:
         return None
     return {
         "metric": "anchored+aligned Mbp/sec at 1/2/4/8 MI355X; bit-exact anchor set vs CPU",
-        "value": round(value, 3), "unit": "Mbp/s", "n_gpus": world, "steps": steps,
+        "value": round(value, 3), "unit": "Mbp/s",
+        "unit_note": "pair bp: every pair's two genomes count (each genome is in %d pairs); the genome "
+                     "set's own rate is input_set_mbp_s" % (synth.CONFIGS[config][0] - 1),
+        "input_set_mbp_s": round(set_bp * steps / dt / 1e6, 3),
+        "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 4),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded, npge_amd/synth.py)",
@@ -310,28 +380,56 @@ def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps,
     }
 
 
-def cpu_baseline_pair(names, seqs, idx, runs):
-    """The oracle's DraftPangenome on one genome pair of the job (a bounded
-    sample of the pair workload), one thread, median of `runs` after a warm-up."""
-    import statistics
+def _oracle_pair_seconds(args):
+    """One genome pair through the oracle's DraftPangenome, 1 thread (runs in
+    a spawned worker process of cpu_baseline_pair's allotted-cores leg)."""
     import time
     from oracle import oracle as orc
+    orc.use_native()  # the parent built it: the same -march=native library
+    pn, ps = args
+    o = orc.BlockSetOracle(ps, pn, seed=1)
+    t = time.perf_counter()
+    o.apply("DraftPangenome")
+    return time.perf_counter() - t, o.hash()
+
+
+def cpu_baseline_pair(names, seqs, sel, runs):
+    """The oracle's DraftPangenome on genome pairs of the job (a bounded sample
+    of the pair workload): one pair on one thread, median of `runs` (>= 3)
+    after a warm-up; and the allotted-cores leg, as many pairs at once as the
+    job has cores (OMP_NUM_THREADS), one spawned process per pair -- pairs are
+    independent on the CPU too."""
+    import multiprocessing as mp
+    import statistics
+    import time
+    from concurrent.futures import ProcessPoolExecutor
+    from oracle import oracle as orc
     native = orc.use_native()
-    pn, ps = [names[i] for i in idx], [seqs[i] for i in idx]
+    runs = max(3, runs)
+    pn, ps = [names[i] for i in sel[0]], [seqs[i] for i in sel[0]]
     bp = sum(len(s) for s in ps)
-    ts = []
-    for r in range(runs + 1):
-        o = orc.BlockSetOracle(ps, pn, seed=1)
-        t = time.perf_counter()
-        o.apply("DraftPangenome")
-        if r:
-            ts.append(time.perf_counter() - t)
+    ts = [_oracle_pair_seconds((pn, ps))[0] for _ in range(runs + 1)][1:]
     t1 = statistics.median(ts)
+    info = _cpu_info()
+    cores = min(max(1, int(os.environ.get("OMP_NUM_THREADS", info["affinity"]))), info["affinity"], len(sel))
+    batch = [([names[i] for i in idx], [seqs[i] for i in idx]) for idx in sel[:cores]]
+    bbp = sum(len(s) for _, ps_ in batch for s in ps_)
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
+    # a worker that dies raises BrokenProcessPool here instead of hanging
+    with ProcessPoolExecutor(max_workers=cores, mp_context=ctx) as pool:
+        list(pool.map(_oracle_pair_seconds, batch))  # warm-up: the workers load the oracle
+        t = time.perf_counter()
+        list(pool.map(_oracle_pair_seconds, batch))
+        tn = time.perf_counter() - t
     return {"value": round(bp / 1e6 / t1, 4), "unit": "Mbp/s", "cores": 1, "kind": "port",
             "sample": "one genome pair of the job (%s, %d bp), DraftPangenome, oracle/ C++ %s, 1 thread, "
                       "median of %d runs after 1 warm-up" % ("+".join(pn), bp,
                                                             "-O3 -march=native" if native else "-O3", runs),
-            "workload": "DraftPangenome", "seconds": round(t1, 3), "host": _cpu_info()}
+            "workload": "DraftPangenome", "seconds": round(t1, 3), "runs_s": [round(x, 3) for x in ts],
+            "host": info,
+            "allotted_cores": {"value": round(bbp / 1e6 / tn, 4), "cores": cores, "seconds": round(tn, 3),
+                               "sample": "the job's first %d pairs (%d bp) at once, one process per pair "
+                                         "(1 thread each), after a warm-up pass" % (cores, bbp)}}
 
 
 def pmc_traffic(kernel, config):

@@ -181,6 +181,9 @@ int npgx_rccl_unique_id(void* out);
 int npgx_rccl_comm_create(const void* unique_id, int32_t rank, int32_t world, int32_t device,
                           npgx_comm** out);
 void npgx_rccl_comm_free(npgx_comm* comm);
+/* the rank count RCCL itself reports for a communicator made by
+ * npgx_rccl_comm_create (ncclCommCount); bench.py puts it in its line */
+int npgx_rccl_comm_count(const npgx_comm* comm, int32_t* n);
 /* Runs every collective of comm on small device buffers and checks the
  * results (a start-up check of a multi-GPU run; collective on all ranks). */
 int npgx_comm_check(const npgx_comm* comm);
@@ -358,6 +361,17 @@ int npgx_blockset_counts(const npgx_blockset* b, int64_t* n_blocks, int64_t* n_f
 int npgx_blockset_copy(const npgx_blockset* b, int64_t* block_start, int32_t* seq,
                        int64_t* min_pos, int64_t* max_pos, int8_t* ori, int64_t* row_off,
                        char* rows);
+/* A 64-bit digest of every gapped row, each bound to its fragment, computed on
+ * the device (no row crosses PCIe); it pins the gap columns the way
+ * npgx_blockset_hash pins the coordinates (rows as RawWrite writes them,
+ * src/algo/RawWrite.cpp:40-59).  With sm(x) = splitmix64's output function of
+ * x + 0x9E3779B97F4A7C15 and, per fragment with a row (seq = input index),
+ *   key = sm(sm(sm(2 * seq + (ori > 0)) + min) + max),
+ *   digest = sum over those rows of [ sm(key + len)
+ *            + sum over columns c of sm(key ^ (c << 8 | row[c])) ]  (mod 2^64).
+ * Independent of the block order; blocks without rows add nothing.  No
+ * reference counterpart (tests/helpers.py restates it in numpy). */
+int npgx_blockset_rows_digest(npgx_blockset* b, uint64_t* digest);
 /* blockset_hash (src/model/block_hash.cpp:112-130) */
 int npgx_blockset_hash(const npgx_blockset* b, uint64_t* hash);
 /* ConSeq (replaces ConSeq::process_block_impl, src/algo/ConSeq.cpp:37-50):

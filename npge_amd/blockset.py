@@ -61,6 +61,7 @@ def _bind(L):
     L.npgx_blockset_counts.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.npgx_blockset_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
     L.npgx_blockset_hash.argtypes = [vp, P(ctypes.c_uint64)]
+    L.npgx_blockset_rows_digest.argtypes = [vp, P(ctypes.c_uint64)]
     L.npgx_blockset_conseq.argtypes = [vp, vp, vp, P(i64), P(i64)]
     L.npgx_blockset_deconseq.argtypes = [vp, vp, vp]
     L.npgx_blockset_stats.argtypes = [vp, P(BbStats)]
@@ -218,6 +219,13 @@ class BlockSetEngine:
     def hash(self):
         h = ctypes.c_uint64()
         _capi.check(_capi.lib().npgx_blockset_hash(self._h, ctypes.byref(h)))
+        return h.value
+
+    def rows_digest(self):
+        """npgx_blockset_rows_digest: a device-computed 64-bit digest of every
+        gapped row bound to its fragment (tests/helpers.py restates it)."""
+        h = ctypes.c_uint64()
+        _capi.check(_capi.lib().npgx_blockset_rows_digest(self._h, ctypes.byref(h)))
         return h.value
 
     def stats(self):

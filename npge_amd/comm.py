@@ -126,6 +126,10 @@ class TorchComm:
     def pointer(self):
         return ctypes.byref(self.struct)
 
+    def count(self):
+        """The process group's rank count."""
+        return self.dist.get_world_size(self.group)
+
 
 class RcclComm:
     """npgx_comm owned by the library: RCCL over xGMI, one process per GPU.
@@ -143,6 +147,7 @@ class RcclComm:
                                                 ctypes.POINTER(vp)]
             L.npgx_rccl_comm_free.argtypes = [vp]
             L.npgx_rccl_comm_free.restype = None
+            L.npgx_rccl_comm_count.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
             L._rccl_bound = True
         self._L = L
         self.errors = []
@@ -161,6 +166,13 @@ class RcclComm:
 
     def pointer(self):
         return self._h
+
+    def count(self):
+        """The rank count RCCL reports for this communicator (ncclCommCount)."""
+        from . import _capi
+        n = ctypes.c_int32()
+        _capi.check(self._L.npgx_rccl_comm_count(self._h, ctypes.byref(n)))
+        return n.value
 
     def close(self):
         if getattr(self, "_h", None):

@@ -449,6 +449,8 @@ struct Fills {
     int n = 0;
     void add(void* p, int64_t bytes, uint32_t v) {
         if (bytes <= 0) return;
+        NPGX_REQUIRE(n < (int)(sizeof(a.op) / sizeof(a.op[0])), NPGX_ERR_STATE,
+                     "k_fill_multi: more resets than one launch holds (launch() before adding more)");
         a.op[n++] = FillOp{(uint32_t*)p, bytes / 4, v};
     }
     void launch(hipStream_t st) {

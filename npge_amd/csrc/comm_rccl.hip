@@ -39,7 +39,8 @@ extern "C" {
 static int cb_allreduce_i32(void* user, int32_t* dev, int64_t n, int32_t op) {
     RcclState* S = (RcclState*)user;
     if (n == 0) return 0;
-    if (hipSetDevice(S->device) != hipSuccess) return -1;
+    DeviceGuard dg(S->device);
+    if (!dg.ok) return -1;
     if (rccl_ok(ncclAllReduce(dev, dev, (size_t)n, ncclInt32, op == NPGX_OP_MIN ? ncclMin : ncclSum, S->comm,
                               S->stream),
                 "ncclAllReduce"))
@@ -50,7 +51,8 @@ static int cb_allreduce_i32(void* user, int32_t* dev, int64_t n, int32_t op) {
 static int cb_allgather_i64(void* user, int64_t value, int64_t* out) {
     RcclState* S = (RcclState*)user;
     int world = 0;
-    if (hipSetDevice(S->device) != hipSuccess) return -1;
+    DeviceGuard dg(S->device);
+    if (!dg.ok) return -1;
     if (rccl_ok(ncclCommCount(S->comm, &world), "ncclCommCount")) return -1;
     if (hipMemcpyAsync(S->one.p, &value, 8, hipMemcpyHostToDevice, S->stream) != hipSuccess) return -1;
     if (rccl_ok(ncclAllGather(S->one.p, S->all.p, 1, ncclInt64, S->comm, S->stream), "ncclAllGather")) return -1;
@@ -61,7 +63,8 @@ static int cb_allgather_i64(void* user, int64_t value, int64_t* out) {
 static int cb_allgatherv_u64(void* user, const uint64_t* dev_in, const int64_t* counts, uint64_t* dev_out) {
     RcclState* S = (RcclState*)user;
     int world = 0, rank = 0;
-    if (hipSetDevice(S->device) != hipSuccess) return -1;
+    DeviceGuard dg(S->device);
+    if (!dg.ok) return -1;
     if (rccl_ok(ncclCommCount(S->comm, &world), "ncclCommCount")) return -1;
     if (rccl_ok(ncclCommUserRank(S->comm, &rank), "ncclCommUserRank")) return -1;
     if (rccl_ok(ncclGroupStart(), "ncclGroupStart")) return -1;
@@ -102,7 +105,8 @@ int npgx_rccl_comm_create(const void* unique_id, int32_t rank, int32_t world, in
     return guard([&] {
         NPGX_REQUIRE(unique_id && out, NPGX_ERR_ARG, "null argument");
         NPGX_REQUIRE(world >= 1 && rank >= 0 && rank < world, NPGX_ERR_ARG, "bad rank / world");
-        NPGX_HIP(hipSetDevice(device));
+        DeviceGuard dg(device);
+        NPGX_REQUIRE(dg.ok, NPGX_ERR_HIP, "hipSetDevice failed");
         auto* S = new RcclState;
         S->device = device;
         try {
@@ -127,6 +131,17 @@ int npgx_rccl_comm_create(const void* unique_id, int32_t rank, int32_t world, in
         c->allgather_i64 = cb_allgather_i64;
         c->allgatherv_u64 = cb_allgatherv_u64;
         *out = c;
+    });
+}
+
+int npgx_rccl_comm_count(const npgx_comm* c, int32_t* n) {
+    return guard([&] {
+        NPGX_REQUIRE(c && c->user && n, NPGX_ERR_ARG, "null argument");
+        auto* S = (RcclState*)c->user;
+        int w = 0;
+        const ncclResult_t r = ncclCommCount(S->comm, &w);
+        NPGX_REQUIRE(r == ncclSuccess, NPGX_ERR_HIP, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+        *n = w;
     });
 }
 
@@ -183,7 +198,7 @@ void npgx_rccl_comm_free(npgx_comm* c) {
     if (!c) return;
     auto* S = (RcclState*)c->user;
     if (S) {
-        (void)hipSetDevice(S->device);
+        DeviceGuard dg(S->device);
         if (S->comm) ncclCommDestroy(S->comm);
         if (S->stream) (void)hipStreamDestroy(S->stream);
         delete S;

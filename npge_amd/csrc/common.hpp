@@ -204,6 +204,23 @@ struct StageTimer {
 
 int current_device_checked();
 
+// Makes `device` current for the guard's scope and restores the calling
+// thread's previous device on every exit path (a collective callback must not
+// move the caller's later HIP work to the communicator's device).
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(device) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 // Small persistent host thread pool for the block bookkeeping that is
 // independent per block (hashing).  run(n, f) calls f(i) for i < n on the
 // workers and the calling thread and returns when all are done.

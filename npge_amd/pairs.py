@@ -33,7 +33,11 @@ import numpy as np
 #   w0 = pair << 44 | block << 12 | local_seq << 1 | (ori > 0)
 #   w1 = min << 32 | max
 PAIR_BITS, BLOCK_BITS, SEQ_BITS = 20, 32, 11
-# per-pair summary record (2 x u64): (pair << 32 | n_blocks), blockset hash
+# per-pair summary record (SUMMARY_WORDS x u64): (pair << 32 | n_blocks),
+# blockset hash (coordinates, block_hash.cpp:112-130), rows digest (every
+# gapped row bound to its fragment, npgx_blockset_rows_digest) -- the gather
+# carries the gap columns' fingerprint beside the coordinates
+SUMMARY_WORDS = 3
 
 
 def genomes_of(names):
@@ -139,16 +143,23 @@ class PairJobs:
         self.device = device
         self.gather_device = gather_device
         self.pair_bp = [sum(len(seqs[i]) for i in self.pairs[p]) for p in range(len(self.pairs))]
-        # worker w runs the rank's pairs w, w + workers, ... one after another,
-        # all on the aligner of its first pair (npgx_blockset_create_sharing):
-        # device memory is one aligner's scratch per worker, not per pair
+        # worker w runs the rank's pairs owner[k] == w one after another, all on
+        # the aligner and AnchorFinder handle of its first pair
+        # (npgx_blockset_create_sharing): device memory is one aligner's
+        # scratch per worker, not per pair.  One mapping decides both the
+        # lender and the schedule (_run_pairs asserts it).
+        self.owner = [k % self.workers for k in range(len(self.mine))]
         self.jobs = []
+        first = {}
         for k, p in enumerate(self.mine):
             idx = self.pairs[p]
             pn, ps = [names[i] for i in idx], [seqs[i] for i in idx]
             ss = _capi.SeqSet(ps, pn)
-            lender = self.jobs[k % self.workers][2] if k >= self.workers else None
+            w = self.owner[k]
+            lender = self.jobs[first[w]][2] if w in first else None
+            first.setdefault(w, k)
             self.jobs.append((p, ss, BlockBuild(ss, pn, ps, lender=lender)))
+        self.ktimes = [None] * len(self.jobs)
         self.records = None
         self.summary = None
 
@@ -168,10 +179,13 @@ class PairJobs:
         def worker(w):
             try:
                 _capi.check(_capi.lib().npgx_set_device(self.device))
-                for k in range(w, len(self.jobs), self.workers):
+                for k in [k for k in range(len(self.jobs)) if self.owner[k] == w]:
                     if errors:
                         return
                     infos[k] = self.jobs[k][2].run()
+                    # this pair's own kernel times: the handles it borrowed are
+                    # reused by the worker's next pair
+                    self.ktimes[k] = self.jobs[k][2].kernel_times()
                     recs[k] = self._records(k)  # packed on the worker, overlapping the others' pairs
             except Exception as e:  # re-raised on the calling thread
                 errors.append(e)
@@ -194,7 +208,7 @@ class PairJobs:
         p, _, job = self.jobs[k]
         bs, seq, mn, mx, ori = job.eng.fragments()
         return (pack_fragments(p, bs, seq, mn, mx, ori),
-                np.array([(p << 32) | (len(bs) - 1), job.eng.hash()], dtype=np.uint64))
+                np.array([(p << 32) | (len(bs) - 1), job.eng.hash(), job.eng.rows_digest()], dtype=np.uint64))
 
     def local_records(self):
         recs = [self._records(k) for k in range(len(self.jobs))]
@@ -224,7 +238,7 @@ class PairJobs:
         return {"pairs": len(self.pairs), "pairs_rank": len(self.jobs), "workers": self.workers,
                 "ms_pairs": round((t1 - t0) * 1e3, 3), "ms_gather": round((t2 - t1) * 1e3, 3),
                 "host_cores_busy": round(cores_busy, 2),
-                "gathered_fragments": int(len(frs) // 2), "gathered_pairs": int(len(sums) // 2),
+                "gathered_fragments": int(len(frs) // 2), "gathered_pairs": int(len(sums) // SUMMARY_WORDS),
                 "stem_blocks": int(sum(i["stem_blocks"] for i in done)),
                 "aligned_residues": int(sum(i["aligned_residues"] for i in done)),
                 "align_jobs": int(sum(i["align_jobs"] for i in done)),
@@ -236,5 +250,22 @@ class PairJobs:
 
     def hashes(self):
         """{pair: blockset hash} of the gathered summaries (after run())."""
-        s = self.summary.reshape(-1, 2)
-        return {int(a >> 32): int(h) for a, h in s.tolist()}
+        s = self.summary.reshape(-1, SUMMARY_WORDS)
+        return {int(r[0] >> 32): int(r[1]) for r in s.tolist()}
+
+    def row_digests(self):
+        """{pair: rows digest} of the gathered summaries (after run())."""
+        s = self.summary.reshape(-1, SUMMARY_WORDS)
+        return {int(r[0] >> 32): int(r[2]) for r in s.tolist()}
+
+    def kernel_times(self):
+        """Per-kernel totals over the rank's pairs of the last run(), each pair's
+        times collected on its worker right after that pair ran."""
+        agg = {}
+        for kts in self.ktimes:
+            for k in kts or []:
+                a = agg.setdefault(k["name"], {"name": k["name"], "ms": 0.0, "bytes": 0.0, "launches": 0})
+                a["ms"] += k["ms"]
+                a["bytes"] += k["bytes"]
+                a["launches"] += k["launches"]
+        return list(agg.values())

@@ -124,3 +124,36 @@ def oracle_anchor_loop(o, workers=1):
     o.deconseq(oc)
     o.apply("Align")
     return st
+
+
+_GOLD = 0x9E3779B97F4A7C15
+_M64 = (1 << 64) - 1
+
+
+def _sm(x):
+    """splitmix64 output of x + golden ratio, vectorised over uint64 arrays."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = np.asarray(x, dtype=np.uint64) + np.uint64(_GOLD)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def rows_digest(blocks):
+    """npgx_blockset_rows_digest restated (include/npge_amd.h): blocks are lists
+    of (seq, min, max, ori, row); every row bound to its fragment's key,
+    summed mod 2^64, independent of the block order."""
+    import numpy as np
+    total = 0
+    for b in blocks:
+        for (q, mn, mx, ori, row) in b:
+            if row is None:
+                continue
+            key = int(_sm(int(_sm(int(_sm(2 * q + (1 if ori > 0 else 0))) + mn) & _M64) + mx) & _M64)
+            r = np.frombuffer(row.encode(), dtype=np.uint8).astype(np.uint64)
+            c = np.arange(len(r), dtype=np.uint64)
+            with np.errstate(over="ignore"):
+                cells = _sm(np.uint64(key) ^ ((c << np.uint64(8)) | r))
+                total = (total + int(_sm((key + len(r)) & _M64)) + int(cells.sum(dtype=np.uint64))) & _M64
+    return total

@@ -52,3 +52,17 @@ def test_bench_two_ranks_gloo(mode):
         assert d["replicas"]["value"] > 0 and d["replicas"]["scaling"] == "weak"
     else:                  # the secondary one-set sharded measurement
         assert d["sharded"]["value"] > 0 and d["sharded"]["scaling"] == "strong"
+
+
+def test_bench_gpus_two_self_launched():
+    """--gpus 2 with no launcher: bench.py starts the two ranks itself."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--config", "small",
+           "--dist-backend", "gloo", "--no-cpu-baseline", "--no-pairs-line", "--no-replicas-line"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["comm_ranks"] == 2 and d["launcher"].startswith("bench.py")
+    assert abs(d["value"] - d["config"]["bp_per_rank"] * 2 / (d["ms_per_step"] / 1e3) / 1e6) / d["value"] < 1e-3

@@ -93,12 +93,17 @@ def test_gather_over_gloo(world):
         assert pairs.unpack_fragments(got) == want
 
 
-def test_pair_cpu_baseline_record():
+def test_pair_cpu_baseline_record(monkeypatch):
     """bench.py's CPU leg for the pair job: the oracle's DraftPangenome on one
-    pair, timed (no GPU); the record names its sample and cores."""
+    pair, timed (no GPU), median of >= 3 runs; and the allotted-cores leg, as
+    many pairs at once as cores in spawned processes.  The record names its
+    samples and cores."""
     import bench
     names, seqs = synth.genome_set("tiny")
-    idx = pairs.all_pairs(names)[0]
-    r = bench.cpu_baseline_pair(names, seqs, idx, 1)
-    assert r["value"] > 0 and r["cores"] == 1 and r["kind"] == "port"
+    sel = pairs.all_pairs(names)
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    r = bench.cpu_baseline_pair(names, seqs, sel, 1)
+    assert r["value"] > 0 and r["cores"] == 1 and r["kind"] == "port" and len(r["runs_s"]) == 3
     assert "G01" in r["sample"] and "G02" in r["sample"] and r["workload"] == "DraftPangenome"
+    a = r["allotted_cores"]
+    assert a["value"] > 0 and a["cores"] == min(2, len(sel))

@@ -1,9 +1,11 @@
 """Pair-sharded block build (npge_amd/pairs.py, BASELINE C4's split) on the
 GPU: every genome pair's DraftPangenome, run several pairs at a time on their
 own host threads and streams, equals the CPU restatement's DraftPangenome on
-that pair (blockset hash and fragment coordinates); the concurrent run equals
-the one-at-a-time run; and the pair jobs split over 2 gloo ranks on the box's
-GPU gather to the one-rank records on every rank."""
+that pair (blockset hash, fragment coordinates AND gapped rows: the rows
+themselves and the device rows digest the gather carries); the 12-worker
+concurrent run (shared aligner scratch) equals the one-at-a-time run row for
+row; and the pair jobs split over 2 gloo ranks on the box's GPU gather to the
+one-rank records on every rank."""
 import os
 import socket
 
@@ -12,6 +14,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from npge_amd import pairs, synth
+from helpers import rows_digest
 
 pytestmark = pytest.mark.gpu
 
@@ -31,8 +34,8 @@ def _oracle_pair(names, seqs, idx):
     return o
 
 
-def _canon(blocks):
-    return sorted(tuple(sorted(f[:4] for f in b)) for b in blocks)
+def _canon(blocks, rows=False):
+    return sorted(tuple(sorted(f if rows else f[:4] for f in b)) for b in blocks)
 
 
 @pytest.mark.parametrize("workers", [1, 3])
@@ -43,27 +46,38 @@ def test_pairs_equal_oracle(workers):
     info = job.run()
     assert info["gathered_pairs"] == 10          # one rank: its records are the whole job
     assert info["stem_blocks"] > 0 and info["aligned_residues"] > 0
+    digests = job.row_digests()
     for p, _, bb in job.jobs:
         o = _oracle_pair(names, seqs, job.pairs[p])
+        ob = o.blocks()
         assert bb.eng.hash() == o.hash(), "pair %d" % p
-        assert _canon(bb.eng.blocks()) == _canon(o.blocks()), "pair %d" % p
+        assert _canon(bb.eng.blocks(), rows=True) == _canon(ob, rows=True), "pair %d" % p
+        # the gathered summary's device digest is the oracle rows' digest
+        assert digests[p] == bb.eng.rows_digest() == rows_digest(ob), "pair %d" % p
 
 
 def test_pairs_concurrent_equal_sequential_c4():
     names, seqs = synth.genome_set("C4")
-    sample = pairs.all_pairs(names)[:5]          # 2 x 5 Mbp each, 2 % divergence
+    sample = pairs.all_pairs(names)[:24]         # 2 x 5 Mbp each, 2 % divergence
     a = pairs.PairJobs(names, seqs, workers=1, pairs=sample)
-    b = pairs.PairJobs(names, seqs, workers=5, pairs=sample)
+    b = pairs.PairJobs(names, seqs, workers=12, pairs=sample)  # the bench's 12 workers, shared scratch
     ia, ib = a.run(), b.run()
     assert ia["aligned_residues"] == ib["aligned_residues"] > 0
     ra, rb = a.local_records(), b.local_records()
+    # coordinates, blockset hashes and rows digests of every pair
     assert np.array_equal(ra[0], rb[0]) and np.array_equal(ra[1], rb[1])
+    assert a.row_digests() == b.row_digests() and len(set(a.row_digests().values())) == len(sample)
     # a second pass over the same resident pairs does the identical work
     b.run()
-    assert np.array_equal(b.local_records()[0], ra[0])
-    # one C4 pair against the CPU restatement
-    o = _oracle_pair(names, seqs, sample[0])
-    assert a.jobs[0][2].eng.hash() == o.hash()
+    assert np.array_equal(b.local_records()[0], ra[0]) and b.row_digests() == a.row_digests()
+    # two C4 pairs against the CPU restatement, rows included
+    for k in (0, 13):
+        o = _oracle_pair(names, seqs, sample[k])
+        ob = o.blocks()
+        eng = b.jobs[k][2].eng
+        assert eng.hash() == o.hash()
+        assert eng.rows_digest() == rows_digest(ob)
+        assert _canon(eng.blocks(), rows=True) == _canon(ob, rows=True)
 
 
 def _worker(rank, world, port, out):
@@ -93,9 +107,10 @@ def test_pairs_sharded_gather_equals_single():
     one.run()
     frs, sums = one.local_records()
     want_f = pairs.unpack_fragments(frs)
-    want_h = {int(a >> 32): int(h) for a, h in sums.reshape(-1, 2).tolist()}
+    want_h = {int(r[0] >> 32): (int(r[1]), int(r[2])) for r in sums.reshape(-1, pairs.SUMMARY_WORDS).tolist()}
     assert out[0][2] + out[1][2] == 10
     for r in range(world):
         rec, summ, _ = out[r]
         assert pairs.unpack_fragments(rec) == want_f
-        assert {int(a >> 32): int(h) for a, h in summ.reshape(-1, 2).tolist()} == want_h
+        assert {int(r[0] >> 32): (int(r[1]), int(r[2]))
+                for r in summ.reshape(-1, pairs.SUMMARY_WORDS).tolist()} == want_h

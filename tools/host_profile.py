@@ -16,11 +16,17 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 L = _capi.lib()
 _capi.check(L.npgx_set_device(0))
-names, seqs = synth.genome_set(cfg)
+if cfg.endswith(":pair"):  # the first genome pair of a config (the pair-sharded job's unit)
+    from npge_amd import pairs as _pairs
+    names, seqs = synth.genome_set(cfg.split(":")[0])
+    idx = _pairs.all_pairs(names)[0]
+    names, seqs = [names[i] for i in idx], [seqs[i] for i in idx]
+else:
+    names, seqs = synth.genome_set(cfg)
 ss = _capi.SeqSet(seqs, names)
 job = pipeline.BlockBuild(ss, names, seqs, anchor_loop=len(sys.argv) > 3 and sys.argv[3] == "alf")
 job.run()
-out = os.path.abspath("gpurun_out/host_prof_%s.txt" % cfg)
+out = os.path.abspath("gpurun_out/host_prof_%s.txt" % cfg.replace(":", "_"))
 os.makedirs(os.path.dirname(out), exist_ok=True)
 L.npgx_diag_prof_start(4000)
 for _ in range(steps):

@@ -15,6 +15,10 @@ for cfg in C3 C2 C4:pair; do
   timeout -k 10 300 python tools/host_profile.py $cfg 10 > $O/host_$cfg.txt 2>&1 || { tail -5 $O/host_$cfg.txt; exit 1; }
   head -40 $O/host_$cfg.txt
 done
+step split_debug_c3
+NPGX_SPLIT_DEBUG=1 NPGX_JOB_STATS=1 NPGX_PREP_DEBUG=1 timeout -k 10 300 python tools/analyze_bb.py C3 > $O/split_debug_c3.txt 2>&1 || { tail -5 $O/split_debug_c3.txt; exit 1; }
+step align_timeline_c3
+timeout -k 10 300 python tools/align_timeline.py C3 > $O/align_timeline_c3.txt 2>&1 || { tail -5 $O/align_timeline_c3.txt; exit 1; }
 step analyze_c3
 timeout -k 10 300 python tools/analyze_bb.py C3 > $O/analyze_c3.txt 2>&1 || { tail -5 $O/analyze_c3.txt; exit 1; }
 step rocprof_c3

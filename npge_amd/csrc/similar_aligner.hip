@@ -65,8 +65,9 @@ struct SaSplit {
     int64_t tgt;        // first int of its sync states (K - 1 states x n rows)
     int32_t seg0;       // its first segment task
     int32_t win;        // half-width of the sync word search window
-    int32_t sub;        // -1: the job's own rows; else the job's sub-job (a bad region) of this index
-    int32_t pad;
+    int32_t sub;        // -1: the job's own rows; -2: a twin (the job's rows reversed, see
+                        // "Twins"); else the job's sub-job (a bad region) of this index
+    int32_t twin;       // job splits: 1 + index of the job's twin split, 0: none
     int64_t post;       // >= 0: byte offset of k_split_post's global work area (chains too long for LDS)
 };
 
@@ -149,6 +150,10 @@ struct SaArgs {
     const int64_t* bits_off;   // ... their first word
     const int32_t* part0;      // per job split: its first k_chain_copy workgroup (n_splits + 1 entries)
     int32_t split_len;         // segment length for a job of 16 rows (0: no splitting)
+    // twins (split jobs' reversed rows, walked beside the jobs): the reversed
+    // copies, at twin_off[row] for the rows of jobs with a twin
+    const char* twin_rows;
+    const int64_t* twin_off;
     int32_t cap_splits, cap_segs;
     int64_t cap_tgt, cap_find, cap_pool;
 };
@@ -1067,7 +1072,10 @@ __host__ __device__ __forceinline__ int seg_cap_for(int mx, int k, int K, int wi
 // reversed bad-region row of one of its sub-jobs (in the job's C)
 __device__ __forceinline__ void split_row(const SaArgs& a, const SaSplit& sp, const SaJob& job, int lane,
                                           const char*& p, int& len) {
-    if (sp.sub < 0) {
+    if (sp.sub == -2) {  // a twin: the job's row reversed
+        p = a.twin_rows + a.twin_off[job.row0 + lane];
+        len = a.row_len[job.row0 + lane];
+    } else if (sp.sub < 0) {
         p = a.rows + a.row_off[job.row0 + lane];
         len = a.row_len[job.row0 + lane];
     } else {
@@ -1657,6 +1665,14 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
                     d.out_cap = oc;
                     d.pad = rg.y - rg.x + 1;  // > 0: its rows are k_sub_rows' to write
                     d.out_off = off + pb - by;
+                    if (sp.twin > 0 && rg.x == 0 && rg.y == L0 - 1) {
+                        // the whole job is one bad region: its rows gap-filtered
+                        // and reversed are the job's input rows reversed, whose
+                        // walk the twin has done (k_twin_post takes it over;
+                        // a negative width keeps k_sub_rows / k_plan_subs off)
+                        d.pad = -d.pad;
+                        ((SaSplit*)a.splits)[sp.twin - 1].sub = sn;
+                    }
                     a.subs[sn] = d;
                     jr[ri] = make_int4(rg.x, rg.y, -(sn + 1), rg.w);
                 }
@@ -1739,6 +1755,7 @@ __global__ __launch_bounds__(256) void k_plan_subs(SaArgs a) {
     unsigned long long* pool_ctr = (unsigned long long*)(a.sctr + SC_POOL_LO);
     for (unsigned int sn = blockIdx.x * blockDim.x + threadIdx.x; sn < n_sub; sn += gridDim.x * blockDim.x) {
         const SaSub d = a.subs[sn];
+        if (d.pad < 0) continue;  // a twin's walk is this sub-job's re-alignment (k_twin_post)
         const SaJob job = a.jobs[d.job];
         const int n = job.n;
         const int* lens = (const int*)(a.pool + d.out_off);
@@ -1769,7 +1786,7 @@ __global__ __launch_bounds__(256) void k_plan_subs(SaArgs a) {
                 sp.seg0 = (int32_t)s0;
                 sp.win = win;
                 sp.sub = (int32_t)sn;
-                sp.pad = 0;
+                sp.twin = 0;
                 sp.post = -1;
                 ((SaSplit*)a.splits)[si] = sp;
             }
@@ -1797,14 +1814,19 @@ __global__ __launch_bounds__(256) void k_plan_subs(SaArgs a) {
 // segments into the sub-job's output (rows of out_cap) and its identical
 // columns (score_of after the re-alignment) -- what k_align_sub writes for a
 // whole sub-job; a chain that overflowed or does not fit: (-1, 0).
-__global__ __launch_bounds__(POST_THREADS) void k_sub_post(SaArgs a, int first) {
+// Twins (k_twin_post, `last` >= 0: the twin splits [first, last)): a twin
+// whose job k_split_post found to be one bad region (sp.sub >= 0) chains into
+// that sub-job's output; when its chain fails the sub-job goes back to the
+// ordinary path (its width restored: k_sub_rows, k_plan_subs, k_align_sub).
+__global__ __launch_bounds__(POST_THREADS) void k_sub_post(SaArgs a, int first, int last_twin) {
     __shared__ int pk[SPLIT_KMAX], pcols[SPLIT_KMAX], pdst[SPLIT_KMAX];
     __shared__ int s_np, s_L, s_fail, s_scan[POST_THREADS / 64];
     const int tid = threadIdx.x;
-    const int last = (int)min(a.sctr[SC_SPLITS], (unsigned int)a.cap_splits);
+    const bool twins = last_twin >= 0;
+    const int last = twins ? last_twin : (int)min(a.sctr[SC_SPLITS], (unsigned int)a.cap_splits);
     for (int si = first + blockIdx.x; si < last; si += gridDim.x) {
         const SaSplit sp = a.splits[si];
-        if (sp.K < 2) continue;
+        if (sp.K < 2 || sp.sub < 0) continue;  // (a twin its job did not need)
         const SaSub d = a.subs[sp.sub];
         const int n = a.jobs[d.job].n;
         __syncthreads();
@@ -1829,7 +1851,10 @@ __global__ __launch_bounds__(POST_THREADS) void k_sub_post(SaArgs a, int first) 
         }
         __syncthreads();
         if (s_fail) {
-            if (tid == 0) a.sub_res[sp.sub] = make_int2(-1, 0);
+            if (tid == 0) {
+                if (twins) a.subs[sp.sub].pad = -d.pad;  // the ordinary re-alignment after all
+                else a.sub_res[sp.sub] = make_int2(-1, 0);
+            }
             continue;
         }
         char* out = (char*)(a.pool + d.out_off + 256);
@@ -2012,7 +2037,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         const bool idle = chained && any_lane(w, start < 0);  // no sync state found
         View v0{nullptr, 0, 1};
         if (w.act) {
-            v0.p = a.rows + a.row_off[job.row0 + lane] + start;
+            v0.p = (chained && sp.sub == -2 ? a.twin_rows + a.twin_off[job.row0 + lane]
+                                            : a.rows + a.row_off[job.row0 + lane]) + start;
             v0.len = a.row_len[job.row0 + lane] - start;
         }
         if (a.aligner_type == 0 && !idle) {
@@ -2271,6 +2297,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
     if (lane == 0) atomicMax(a.slot_epoch, epoch);  // the launch's highest epoch
 }
 
+// the reversed copies of the twin jobs' rows (list: their rows' indices)
+__global__ void k_twin_rows(const char* __restrict__ rows, const int64_t* __restrict__ row_off,
+                            const int32_t* __restrict__ row_len, const int32_t* __restrict__ list, int n,
+                            const int64_t* __restrict__ twin_off, char* __restrict__ out) {
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int r = list[i];
+        const char* src = rows + row_off[r];
+        const int L = row_len[r];
+        char* d = out + twin_off[r];
+        for (int c = threadIdx.x; c < L; c += blockDim.x) d[c] = src[L - 1 - c];
+    }
+}
+
 struct GatherRow {
     int64_t out_off;    // output byte offset
     int64_t src;        // device address of the aligned row (0: empty row -> gaps)
@@ -2382,6 +2421,14 @@ struct npgx_aligner {
     // least two rows are cut every `split` columns of their longest row
     // (NPGX_ALIGN_SPLIT; 0: never)
     int split = 384;
+    // twins of the split jobs (NPGX_TWINS: -1 auto = in launches with few
+    // tasks, 0 never, 1 always): see "Twins" at align_device
+    int twins = -1;
+    std::vector<int64_t> h_twin_off;
+    std::vector<int32_t> h_twin_list;
+    DevBuf<char> d_twin;
+    DevBuf<int64_t> d_twin_off;
+    DevBuf<int32_t> d_twin_list;
     // bytes the per-slot scratch of one launch may take (NPGX_SLOT_BUDGET_MB;
     // default 16 GiB: allocating much more costs seconds on first use)
     int64_t slot_budget = 0;
@@ -2649,7 +2696,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 sp.seg0 = (int32_t)segs.size();
                 sp.win = std::min(SPLIT_RMAX, 64 + mx / 128);
                 sp.sub = -1;
-                sp.pad = 0;
+                sp.twin = 0;
                 sp.post = -1;
                 {  // a chain that may outgrow k_split_post's LDS: a global work area
                     const int64_t need = (((int64_t)J.cap + 63) / 64) * 8 + 17ll * (J.cap + 1) + 64;
@@ -2675,6 +2722,60 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 }
                 for (int t = 0; t + 1 < K; t++) ftasks.push_back(make_int2((int)splits.size(), t));
                 splits.push_back(sp);
+            }
+        }
+        // Twins.  fix_bad_regions (SimilarAligner.cpp:428-459) re-aligns a bad
+        // region's rows gap-filtered and reversed; when the whole alignment is
+        // one bad region -- most many-row alignments (at 17 rows and 0.8 %
+        // divergence fewer than 90 % of the columns are identical) -- those
+        // rows are the job's input rows reversed, known before the walk.  In a
+        // launch with few tasks (the last ExtendLoopFast iterations: tens of
+        // long jobs on a GPU of thousands of wave slots) every split job gets
+        // a twin split over its reversed rows whose segments run in the same
+        // k_align_jobs launch; k_split_post hands a whole-job bad region to
+        // the twin (k_twin_post chains it), so the re-alignment no longer
+        // follows the forward walk.  The walk is the same process_seqs either
+        // way (bit-exact); a twin whose chain fails leaves its sub-job to the
+        // ordinary path, an unneeded twin costs only idle slots.
+        const int n_js = (int)splits.size();
+        bool twins = false;
+        if (attempt == 0 && n_js > 0 && al->twins != 0) {
+            const int64_t unsplit = (int64_t)todo.size() - n_js;
+            twins = al->twins > 0 || 2 * (int64_t)segs.size() + unsplit <= 2048;
+        }
+        int64_t twin_bytes = 0;
+        if (twins) {
+            al->h_twin_off.assign(ne_len.size(), 0);
+            al->h_twin_list.clear();
+            for (int si = 0; si < n_js; si++) {
+                SaSplit tw = splits[si];
+                const SaJob& J = jobs[tw.job];
+                for (int i = 0; i < J.n; i++) {
+                    al->h_twin_off[J.row0 + i] = twin_bytes;
+                    al->h_twin_list.push_back((int32_t)(J.row0 + i));
+                    twin_bytes += ne_len[J.row0 + i];
+                }
+                const int ti = (int)splits.size();
+                tw.sub = -2;
+                tw.twin = 0;
+                tw.tgt = n_tgt;
+                tw.seg0 = (int32_t)segs.size();
+                tw.post = -1;
+                n_tgt += (int64_t)(tw.K - 1) * J.n;
+                for (int k = 0; k < tw.K; k++) {
+                    SaSeg g;
+                    g.split = ti;
+                    g.k = k;
+                    g.cap = seg_cap_for(jmax[tw.job], k, tw.K, tw.win, J.cap);
+                    g.pad = 0;
+                    g.out = seg_bytes;
+                    seg_bytes += ((int64_t)J.n * g.cap + 255) & ~255ll;
+                    queue.push_back(-(int32_t)segs.size() - 1);
+                    segs.push_back(g);
+                }
+                for (int t = 0; t + 1 < tw.K; t++) ftasks.push_back(make_int2(ti, t));
+                splits[si].twin = ti + 1;
+                splits.push_back(tw);
             }
         }
         if (splits.empty()) {
@@ -2864,6 +2965,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.qsub = nullptr;
         A.ftasks = nullptr;
         A.split_len = o.aligner_type == 0 ? al->split : 0;
+        A.twin_rows = nullptr;
+        A.twin_off = nullptr;
         A.post_area = nullptr;
         if (post_bytes > 0) {
             al->d_post.grow((size_t)post_bytes);
@@ -2933,7 +3036,22 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A.qseg = al->d_qseg.p;
             A.qsub = al->d_qsub.p;
             A.ftasks = al->d_ftasks.p;
+            if (twins) {
+                al->d_twin.grow((size_t)std::max<int64_t>(twin_bytes, 1));
+                al->d_twin_off.grow(al->h_twin_off.size());
+                al->d_twin_list.grow(al->h_twin_list.size());
+                put(al->d_twin_off.p, al->h_twin_off.data(), al->h_twin_off.size() * 8);
+                put(al->d_twin_list.p, al->h_twin_list.data(), al->h_twin_list.size() * 4);
+                A.twin_rows = al->d_twin.p;
+                A.twin_off = al->d_twin_off.p;
+            }
             flush();
+            if (twins) {
+                hipLaunchKernelGGL(k_twin_rows, dim3((unsigned)std::min<size_t>(al->h_twin_list.size(), 4096)),
+                                   dim3(256), 0, st, d_rows, al->d_row_off.p, al->d_row_len.p, al->d_twin_list.p,
+                                   (int)al->h_twin_list.size(), al->d_twin_off.p, al->d_twin.p);
+                NPGX_HIP(hipGetLastError());
+            }
             if (n_job_find > 0) {
                 size_t tf = al->timer.begin("align_split", st, 0.0, (int64_t)n_job_find);
                 hipLaunchKernelGGL(k_split_find, dim3((unsigned)n_job_find), dim3(64 * SPLIT_WAVES), SPLIT_LDS, st, A,
@@ -2953,22 +3071,28 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->timer.end(ti, st);
         pmark(7);
         if (!splits.empty()) {  // the split jobs: chain, regions, deferred bad regions
-            ti = al->timer.begin("align_split_chain", st, 0.0, (int64_t)splits.size());
-            hipLaunchKernelGGL(k_split_chain, dim3((unsigned)splits.size()), dim3(POST_THREADS), 0, st, A);
+            // (the job splits only: the twins [n_js, splits.size()) are chained by k_twin_post)
+            ti = al->timer.begin("align_split_chain", st, 0.0, (int64_t)n_js);
+            hipLaunchKernelGGL(k_split_chain, dim3((unsigned)n_js), dim3(POST_THREADS), 0, st, A);
             NPGX_HIP(hipGetLastError());
-            hipLaunchKernelGGL(k_chain_copy, dim3((unsigned)part0.back()), dim3(POST_THREADS), 0, st, A,
-                               (int)splits.size());
+            hipLaunchKernelGGL(k_chain_copy, dim3((unsigned)part0.back()), dim3(POST_THREADS), 0, st, A, n_js);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
-            ti = al->timer.begin("align_split_post", st, 0.0, (int64_t)splits.size());
-            hipLaunchKernelGGL(k_split_post, dim3((unsigned)splits.size()), dim3(REG_THREADS), POST_LDS, st, A,
+            ti = al->timer.begin("align_split_post", st, 0.0, (int64_t)n_js);
+            hipLaunchKernelGGL(k_split_post, dim3((unsigned)n_js), dim3(REG_THREADS), POST_LDS, st, A,
                                (int)POST_LDS);
             NPGX_HIP(hipGetLastError());
+            if (twins) {  // k_twin_post: the twins whose jobs are one bad region
+                const int n_tw = (int)splits.size() - n_js;
+                hipLaunchKernelGGL(k_sub_post, dim3((unsigned)std::min(n_tw, 512)), dim3(POST_THREADS), 0, st, A, n_js,
+                                   (int)splits.size());
+                NPGX_HIP(hipGetLastError());
+            }
             al->timer.end(ti, st);
         }
         if (deferring) {  // the deferred bad regions, then their jobs (no-ops when nothing was deferred)
             // jobs that may have deferred: the split ones and the long ones
-            int64_t n_fin = (int64_t)splits.size();
+            int64_t n_fin = (int64_t)n_js;
             int64_t max_rc = 1;
             {
                 std::vector<uint8_t> is_split(n_jobs, 0);
@@ -3003,7 +3127,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             al->timer.end(ti, st);
             if (split_subs) {  // the split sub-jobs' chains
                 ti = al->timer.begin("align_sub_post", st, 0.0, 0);
-                hipLaunchKernelGGL(k_sub_post, dim3(512), dim3(POST_THREADS), 0, st, A, n_job_splits);
+                hipLaunchKernelGGL(k_sub_post, dim3(512), dim3(POST_THREADS), 0, st, A, n_job_splits, -1);
                 NPGX_HIP(hipGetLastError());
                 al->timer.end(ti, st);
             }
@@ -3313,6 +3437,8 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         if (dr && *dr) a->defer_rows = std::max(0, atoi(dr));
         const char* sp = getenv("NPGX_ALIGN_SPLIT");
         if (sp && *sp) a->split = std::max(0, atoi(sp));
+        const char* tw = getenv("NPGX_TWINS");
+        if (tw && *tw) a->twins = atoi(tw) > 0 ? 1 : (atoi(tw) == 0 ? 0 : -1);
         const char* sb = getenv("NPGX_SLOT_BUDGET_MB");
         if (sb && *sb) {
             a->slot_budget = (int64_t)std::max(1, atoi(sb)) << 20;

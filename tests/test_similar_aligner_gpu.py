@@ -192,6 +192,26 @@ def test_split_similar_families(split, monkeypatch):
     _check(jobs)
 
 
+@pytest.mark.parametrize("twins", ["0", "1", "-1"])
+@pytest.mark.parametrize("split", ["128", "384"])
+def test_twins(twins, split, monkeypatch):
+    """Twins (similar_aligner.hip, align_device "Twins"): every split job also
+    walks its reversed rows in the same launch, and a job that turns out to be
+    one bad region takes that walk as its re-alignment (NPGX_TWINS 1: always,
+    0: never, -1: in launches with few tasks).  Families from nearly identical
+    (a good alignment: the twin is not used) to unrelated (one bad region;
+    chains that fail on missed sync states fall back), many rows and two."""
+    monkeypatch.setenv("NPGX_TWINS", twins)
+    monkeypatch.setenv("NPGX_ALIGN_SPLIT", split)
+    rng = np.random.default_rng(41)
+    jobs = []
+    for d in (0.005, 0.02, 0.06, 0.15, 0.4):
+        for n in (2, 5, 17):
+            L = int(rng.integers(1500, 6000))
+            jobs.append(_family(rng, n, L, d, tail_unrelated=float(rng.choice([0.0, 0.3]))))
+    _check(jobs)
+
+
 def test_wide_blocks():
     _check(_random_jobs(12, 20, nmax=64, lmax=200))
 

@@ -8,12 +8,13 @@ export TMPDIR=/tmp
 R=$(pwd)
 TAG=$1; VAR=$2; VA=$3; VB=$4
 shift 4
+SFX=$(echo "$*" | tr -c 'A-Za-z0-9' '_' | cut -c1-40)
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 for rep in 1 2; do
   for v in "$VA" "$VB"; do
-    env $VAR=$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-pairs-line "$@" > $O/ab_${VAR}_${v}_$rep.log 2>&1 || { tail -5 $O/ab_${VAR}_${v}_$rep.log; exit 1; }
-    python - "$O/ab_${VAR}_${v}_$rep.log" "$VAR=$v" <<'PY'
+    env $VAR=$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-pairs-line "$@" > $O/ab_${VAR}_${v}_${SFX}_$rep.log 2>&1 || { tail -5 $O/ab_${VAR}_${v}_${SFX}_$rep.log; exit 1; }
+    python - "$O/ab_${VAR}_${v}_${SFX}_$rep.log" "$VAR=$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 st = d["last_step"]["ms_stage"]

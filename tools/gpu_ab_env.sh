@@ -17,10 +17,15 @@ for rep in 1 2; do
     python - "$O/ab_${VAR}_${v}_${SFX}_$rep.log" "$VAR=$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-st = d["last_step"]["ms_stage"]
-print("%-14s ms/step %.3f value %.1f align %.3f (kernel wait %.3f) host %.3f" % (
-    sys.argv[2], d["ms_per_step"], d["value"], st["align_batch"], st["align_kernel_wait"],
-    d["last_step"]["ms_host_bookkeeping"]))
+ls = d["last_step"]
+if "ms_stage" in ls:
+    st = ls["ms_stage"]
+    print("%-14s ms/step %.3f value %.1f align %.3f (kernel wait %.3f) host %.3f" % (
+        sys.argv[2], d["ms_per_step"], d["value"], st["align_batch"], st["align_kernel_wait"],
+        ls["ms_host_bookkeeping"]))
+else:  # the pair job
+    print("%-14s ms/step %.3f value %.1f pair host %.3f align %.3f" % (
+        sys.argv[2], d["ms_per_step"], d["value"], ls["mean_pair_ms_host"], ls["mean_pair_ms_align"]))
 PY
   done
 done

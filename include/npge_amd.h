@@ -63,6 +63,11 @@ typedef struct {
 int npgx_seqset_create(const char* const* seqs, const int64_t* lens,
                        const char* const* names, int32_t n, npgx_seqset** out);
 int npgx_seqset_count(const npgx_seqset* s, int32_t* n);
+/* wall ms of npgx_seqset_create: the host's to_atgcn (the CPU side's input
+ * conversion, excluded from throughput) and the upload proper -- one DMA of
+ * the ASCII text from pinned staging plus k_pack (H2D included
+ * on the GPU side) */
+int npgx_seqset_timings(const npgx_seqset* s, double* ms_host, double* ms_upload);
 /* size after to_atgcn of input sequence `index` */
 int npgx_seqset_size(const npgx_seqset* s, int32_t index, int64_t* size);
 /* rank of input sequence `index` in the processing order */

@@ -87,6 +87,7 @@ def lib():
     L.npgx_seqset_rank.argtypes = [vp, i32, P(i32)]
     L.npgx_seqset_text.argtypes = [vp, i32, i64, i64, ctypes.c_char_p]
     L.npgx_seqset_device_bytes.argtypes = [vp, P(i64)]
+    L.npgx_seqset_timings.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double)]
     L.npgx_seqset_free.argtypes = [vp]
     L.npgx_seqset_free.restype = None
     L.npgx_af_default_options.argtypes = [P(AfOptions)]
@@ -173,6 +174,12 @@ class SeqSet:
         v = ctypes.c_int64()
         check(lib().npgx_seqset_size(self._h, i, ctypes.byref(v)))
         return v.value
+
+    def timings(self):
+        """(host to_atgcn ms, upload ms = H2D + k_pack) of the creation."""
+        a, b = ctypes.c_double(), ctypes.c_double()
+        check(lib().npgx_seqset_timings(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def rank(self, i):
         v = ctypes.c_int32()

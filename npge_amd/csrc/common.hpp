@@ -302,4 +302,5 @@ struct npgx_seqset {
     std::vector<int64_t> n_off;          // first uint64 word of the N bitmap of rank r
     int64_t total_words = 0, total_nwords = 0;
     npgx::DevBuf<uint64_t> words, nmask;
+    double ms_host = 0, ms_upload = 0;   // npgx_seqset_create: host to_atgcn / H2D + k_pack
 };

@@ -318,26 +318,35 @@ int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char*
             s->names[i] = names && names[i] ? names[i] : "";
             total += lens[i];
         }
+        const auto t0 = std::chrono::steady_clock::now();
         heavy_for((size_t)n, total, [&](size_t i) { s->data[i] = to_atgcn(seqs[i], lens[i]); });
-        // the ASCII text on the device in input order, then packed
+        const auto t1 = std::chrono::steady_clock::now();
+        s->ms_host = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        // the ASCII text on the device in input order (one DMA from pinned
+        // staging kept across calls), then packed by k_pack
         std::vector<int64_t> ascii(n + 1, 0);
         for (int32_t i = 0; i < n; i++) ascii[i + 1] = ascii[i] + (int64_t)s->data[i].size();
         DevBuf<unsigned char> d_ascii;
         d_ascii.ensure((size_t)std::max<int64_t>(ascii[n], 1));
-        if (n <= 256) {  // few (long) sequences: each straight to its place
-            for (int32_t i = 0; i < n; i++)
-                if (!s->data[i].empty())
-                    NPGX_HIP(hipMemcpy(d_ascii.p + ascii[i], s->data[i].data(), s->data[i].size(),
-                                       hipMemcpyHostToDevice));
-        } else if (ascii[n] > 0) {  // many: gathered on host threads, one copy
-            std::unique_ptr<char[]> cat(new char[(size_t)ascii[n]]);
-            heavy_for((size_t)n, ascii[n], [&](size_t i) {
-                memcpy(cat.get() + ascii[i], s->data[i].data(), s->data[i].size());
-            });
-            NPGX_HIP(hipMemcpy(d_ascii.p, cat.get(), (size_t)ascii[n], hipMemcpyHostToDevice));
+        if (ascii[n] > 0) {
+            static std::mutex mu;
+            static PinnedBuf<char> staging;
+            std::lock_guard<std::mutex> lk(mu);
+            char* st = staging.ensure((size_t)ascii[n]);
+            heavy_for((size_t)n, ascii[n], [&](size_t i) { memcpy(st + ascii[i], s->data[i].data(), s->data[i].size()); });
+            NPGX_HIP(hipMemcpy(d_ascii.p, st, (size_t)ascii[n], hipMemcpyHostToDevice));
         }
         pack_device(s.get(), d_ascii.p, ascii);
+        s->ms_upload = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
         *out = s.release();
+    });
+}
+
+int npgx_seqset_timings(const npgx_seqset* s, double* ms_host, double* ms_upload) {
+    return guard([&] {
+        NPGX_REQUIRE(s && ms_host && ms_upload, NPGX_ERR_ARG, "null argument");
+        *ms_host = s->ms_host;
+        *ms_upload = s->ms_upload;
     });
 }
 

@@ -2421,9 +2421,11 @@ struct npgx_aligner {
     // least two rows are cut every `split` columns of their longest row
     // (NPGX_ALIGN_SPLIT; 0: never)
     int split = 384;
-    // twins of the split jobs (NPGX_TWINS: -1 auto = in launches with few
-    // tasks, 0 never, 1 always): see "Twins" at align_device
-    int twins = -1;
+    // twins of the split jobs (NPGX_TWINS: 0 never -- the default: measured at
+    // C3 and C5 the whole-job bad region they serve is rare among split jobs
+    // and their segments slow the launch -- 1 always, -1 in launches with few
+    // tasks): see "Twins" at align_device
+    int twins = 0;
     std::vector<int64_t> h_twin_off;
     std::vector<int32_t> h_twin_list;
     DevBuf<char> d_twin;

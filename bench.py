@@ -286,6 +286,9 @@ def main():
                        "genomes": synth.CONFIGS[args.config][0], "anchor_size": 20,
                        "anchor_fp": 0.1, "max_anchor_fragments": 100000,
                        "inputs": "resident in HBM before the timed region (upload: pcie_inclusive)",
+                       "timers": "HIP events around the k_align_jobs launches only (NPGX_TIMERS=1: every "
+                                 "event is a queue marker that costs the GPU time; per-kernel times of the "
+                                 "rest: the rocprofv3 summaries in profiles/)",
                        "parallelism": ("sharded x%d (one set; %s)" % (world, "library RCCL communicator"
                                                                        if args.dist_backend == "nccl" else
                                                                        args.dist_backend)) if sharded

@@ -9,6 +9,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 
+os.environ.setdefault("NPGX_TIMERS", "2")  # every launch timed (read at handle creation)
+
 os.environ.setdefault("NPGX_JOB_STATS", "1")
 from npge_amd import _capi, synth  # noqa: E402
 from npge_amd.anchor_finder import AnchorFinder  # noqa: E402

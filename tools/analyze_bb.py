@@ -9,6 +9,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 
+os.environ.setdefault("NPGX_TIMERS", "2")  # every launch timed (read at handle creation)
+
 os.environ.setdefault("NPGX_JOB_STATS", "1")  # per-job statistics (read at aligner creation)
 
 from npge_amd import _capi, synth

@@ -1,0 +1,14 @@
+#!/bin/bash
+# full GPU suite + smoke + default bench (tools/round_end.sh tests), then the
+# C3 kernel trace and its step timeline
+set -o pipefail
+export TMPDIR=/tmp
+R=$(pwd)
+tools/round_end.sh r04g tests || exit 1
+O=$R/gpurun_out/r04g
+echo "== rocprof C3 $(date +%T)"
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/prof_c3.log 2>&1 || { tail -5 $O/prof_c3.log; exit 1; }
+cd $R
+python tools/step_timeline.py $O/prof_c3/run_kernel_trace.csv > $O/c3_step_timeline.txt 2>&1
+head -14 $O/c3_step_timeline.txt

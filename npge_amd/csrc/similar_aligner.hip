@@ -2381,7 +2381,9 @@ struct npgx_aligner {
     DevBuf<int64_t> d_row_off;
     DevBuf<int32_t> d_row_len;
     DevBuf<SaJob> d_jobs;
-    DevBuf<int32_t> d_order, d_job_len, d_job_status;
+    // per job: length | status, then the launch's highest word-table epoch --
+    // one array, so the results come back in one copy
+    DevBuf<int32_t> d_order, d_job_out;
     DevBuf<int64_t> d_job_stats;
     std::vector<int64_t> job_stats;
     DevBuf<unsigned int> d_next;
@@ -2390,7 +2392,6 @@ struct npgx_aligner {
     PinnedArena pinned;          // staging of the batch's host<->device copies
     DevBuf<unsigned long long> tkeys, tmask;
     DevBuf<uint32_t> tdone;
-    DevBuf<uint32_t> slot_epoch;
     size_t tcap_alloc = 0;
     uint32_t epoch_base = 1;  // first word-table epoch of the next launch
     DevBuf<const char*> st_p;
@@ -2602,8 +2603,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     al->d_row_len.ensure(ne_len.size());
     al->d_jobs.ensure(jobs.size());
     al->d_order.ensure(order.size());
-    al->d_job_len.ensure(jobs.size());
-    al->d_job_status.ensure(jobs.size());
+    al->d_job_out.ensure(2 * jobs.size() + 1);
+    int32_t* const d_job_len = al->d_job_out.p;
+    int32_t* const d_job_status = d_job_len + jobs.size();
+    uint32_t* const d_slot_epoch = (uint32_t*)(d_job_status + jobs.size());
     al->d_job_stats.ensure(jobs.size() * NPGX_JOB_STATS);
     al->job_stats.assign(al->want_stats ? jobs.size() * NPGX_JOB_STATS : 0, 0);
     al->d_next.ensure(1);
@@ -2835,8 +2838,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             al->tcap_alloc = std::max(al->tcap_alloc, slots * tcap);
             al->epoch_base = 1;
         }
-        al->slot_epoch.ensure(1);
-        zero(al->slot_epoch.p, 4);
+        zero(d_slot_epoch, 4);
         al->st_p.ensure(slots * depth * 64);
         al->st_len.ensure(slots * depth * 64);
         al->st_pos.ensure(slots * depth * 64);
@@ -2855,15 +2857,15 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.n_jobs = nj;
         A.aligner_type = o.aligner_type;
         A.scratch = scr.p;
-        A.job_len = al->d_job_len.p;
-        A.job_status = al->d_job_status.p;
+        A.job_len = d_job_len;
+        A.job_status = d_job_status;
         A.job_stats = al->want_stats ? al->d_job_stats.p : nullptr;
         A.next_job = al->d_next.p;
         A.tkeys = al->tkeys.p;
         A.tmask = al->tmask.p;
         A.tdone = al->tdone.p;
         A.tcap_log2 = tlog;
-        A.slot_epoch = al->slot_epoch.p;
+        A.slot_epoch = d_slot_epoch;
         A.epoch_base = al->epoch_base;
         A.st_p = al->st_p.p;
         A.st_len = al->st_len.p;
@@ -3264,9 +3266,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         }
         pmark(8);
         int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);
-        NPGX_HIP(hipMemcpyAsync(pl, al->d_job_len.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipMemcpyAsync(pl + n_jobs, al->d_job_status.p, n_jobs * 4, hipMemcpyDeviceToHost, st));
-        NPGX_HIP(hipMemcpyAsync(pl + 2 * n_jobs, al->slot_epoch.p, 4, hipMemcpyDeviceToHost, st));
+        NPGX_HIP(hipMemcpyAsync(pl, d_job_len, ((size_t)n_jobs * 2 + 1) * 4, hipMemcpyDeviceToHost, st));
         if (al->want_stats)
             NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
         al->host_ms[0] += ms(tp);

@@ -12,3 +12,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 cd $R
 python tools/step_timeline.py $O/prof_c3/run_kernel_trace.csv > $O/c3_step_timeline.txt 2>&1
 head -14 $O/c3_step_timeline.txt
+echo "== af epochs C3 $(date +%T)"
+timeout -k 10 300 python tools/af_epoch_sweep.py C3 0,4,8,12,16,24 6 > $O/af_epochs_c3.txt 2>&1 || { tail -5 $O/af_epochs_c3.txt; exit 1; }
+cat $O/af_epochs_c3.txt
+for w in 12 16 20; do
+  echo "== pairs workers $w $(date +%T)"
+  timeout -k 10 300 python bench.py --mode pairs --pair-workers $w --steps 2 --warmup 1 --no-cpu-baseline > $O/pairs_w$w.log 2>&1 || { tail -5 $O/pairs_w$w.log; exit 1; }
+  python -c "import json,sys; d=json.loads(open('$O/pairs_w$w.log').read().strip().splitlines()[-1]); print('workers $w', d['value'], d['ms_per_step'], d['last_step']['host_cores_busy'])"
+done

@@ -24,6 +24,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <set>
@@ -2128,10 +2129,15 @@ static void extend_loop_fast(BlockSetO& bs, const PipelineOpts& o, PipelineStats
         // Move target=target other=unchanged
         for (BBlock& b : unchanged) fixed.push_back(std::move(b));
         // OverlaplessUnion target=ol other=target --ou-move:=1
+        const size_t n_ou = fixed.size();
         overlapless_union(fixed);
         // Clear target; Move target=target other=ol; Clear ol
         bs.blocks.swap(fixed);
         uint64_t h = blockset_hash(bs);
+        static const bool dbg = getenv("ORACLE_ELF_DEBUG") != nullptr;  // (diagnostic: per-iteration state)
+        if (dbg)
+            fprintf(stderr, "elf it %d: ou_in %zu kept %zu state %016llx\n", it, n_ou, bs.blocks.size(),
+                    (unsigned long long)h);
         if (seen_states.count(h)) break;
         seen_states.insert(h);
     }

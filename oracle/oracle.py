@@ -438,3 +438,49 @@ class BlockSetOracle:
         if rc != 0:
             raise RuntimeError("oracle DeConSeq failed (%d)" % rc)
         return self
+
+
+def anchor_blocks(r):
+    """AnchorFinder SoA result -> blocks [(seq, min, max, ori, None), ...] in
+    result order (AnchorFinder.cpp:364-390)."""
+    bs = r["block_start"]
+    return [[(int(r["seq"][i]), int(r["min_pos"][i]), int(r["max_pos"][i]), int(r["ori"][i]), None)
+             for i in range(bs[b], bs[b + 1])] for b in range(len(bs) - 1)]
+
+
+def consensus_order(b):
+    """The block order ConSeq sees (ConSeq.cpp:37-50 walks the block set):
+    the reference's is the std::set<Block*> pointer order (BlockSet.hpp:30,
+    arbitrary run to run); pinned here to the sorted fragment coordinates."""
+    return sorted((f[0], f[1], f[2], f[3]) for f in b)
+
+
+def anchor_loop_fast(o, workers=1):
+    """AnchorLoopFast (src/algo/lua_lib.lua:741-758) over this restatement's
+    processors, on BlockSetOracle `o` holding the current blocks:
+      Filter; Rest target=target other=target;
+      ConSeq target=cons other=target (blocks in consensus_order);
+      AnchorFinder target=cons; MoveUnchanged target=null other=cons (a fresh
+      pipe: nothing seen yet, nothing dropped); DummyAligner target=cons;
+      ExtendAndAlign target=cons (FragmentsExtender --extend-length-portion:=0.5,
+      then Align, Align.cpp:36-52); ExtendLoopFast target=cons (its
+      set_max_iterations(-1), lua_lib.lua:697-699);
+      DeConSeq target=target other=cons (DeConSeq.cpp:51-83); Align.
+    Returns the consensus set's stats (its ExtendLoopFast iterations)."""
+    o.apply("Filter")
+    o.apply("Rest")
+    o.set_blocks(sorted(o.blocks(), key=consensus_order))
+    cs = o.conseq()
+    oc = BlockSetOracle(cs, [""] * len(cs), portion_x1e4=5000, max_iterations=-1)
+    if workers > 1:
+        oc.set_workers(workers)
+    oc.set_blocks(anchor_blocks(AnchorFinder().run(cs, [""] * len(cs))))
+    for op in ("DummyAligner", "FragmentsExtender", "Align"):
+        oc.apply(op)
+    it0 = oc.stats()["iterations"]
+    oc.apply("ExtendLoopFast")
+    st = oc.stats()
+    st["iterations"] -= it0
+    o.deconseq(oc)
+    o.apply("Align")
+    return st

@@ -81,49 +81,22 @@ def blocks_digest(blocks):
 
 
 def oracle_anchor_blocks(r):
-    """AnchorFinder SoA result -> blocks [(seq, min, max, ori, None), ...] in
-    result order (AnchorFinder.cpp:364-390)."""
-    bs = r["block_start"]
-    return [[(int(r["seq"][i]), int(r["min_pos"][i]), int(r["max_pos"][i]), int(r["ori"][i]), None)
-             for i in range(bs[b], bs[b + 1])] for b in range(len(bs) - 1)]
+    """(oracle.anchor_blocks)"""
+    from oracle import oracle as orc
+    return orc.anchor_blocks(r)
 
 
 def consensus_order(b):
-    """The block order ConSeq sees on both sides: the reference's is the
-    std::set<Block*> pointer order (arbitrary); the engine pins it to the
-    sorted fragment coordinates (block_build.hip anchor_loop_fast), restated
-    here so that the oracle leg does not borrow the product's convention."""
-    return sorted((f[0], f[1], f[2], f[3]) for f in b)
+    """(oracle.consensus_order: the pinned ConSeq block order)"""
+    from oracle import oracle as orc
+    return orc.consensus_order(b)
 
 
 def oracle_anchor_loop(o, workers=1):
-    """AnchorLoopFast (lua_lib.lua:741-758) over the oracle's processors, on
-    BlockSetOracle `o` holding the DraftPangenome result: Filter, Rest,
-    blocks in consensus_order, ConSeq; on the consensus sequences
-    AnchorFinder -> DummyAligner -> ExtendAndAlign (FragmentsExtender
-    --extend-length-portion:=0.5, Align) -> ExtendLoopFast to convergence;
-    DeConSeq into `o` and Align (Align.cpp:36-52: MetaAligner,
-    SelfOverlapsResolver, MetaAligner, {MoveGaps, CutGaps, Filter} to a
-    fixpoint).  Returns the consensus set's stats (its ExtendLoopFast
-    iterations)."""
+    """AnchorLoopFast over the oracle's processors (oracle.anchor_loop_fast,
+    lua_lib.lua:741-758)."""
     from oracle import oracle as orc
-    o.apply("Filter")
-    o.apply("Rest")
-    o.set_blocks(sorted(o.blocks(), key=consensus_order))
-    cs = o.conseq()
-    oc = orc.BlockSetOracle(cs, [""] * len(cs), portion_x1e4=5000, max_iterations=-1)
-    if workers > 1:
-        oc.set_workers(workers)
-    oc.set_blocks(oracle_anchor_blocks(orc.AnchorFinder().run(cs, [""] * len(cs))))
-    for op in ("DummyAligner", "FragmentsExtender", "Align"):
-        oc.apply(op)
-    it0 = oc.stats()["iterations"]
-    oc.apply("ExtendLoopFast")
-    st = oc.stats()
-    st["iterations"] -= it0
-    o.deconseq(oc)
-    o.apply("Align")
-    return st
+    return orc.anchor_loop_fast(o, workers)
 
 
 _GOLD = 0x9E3779B97F4A7C15

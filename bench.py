@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--mode", choices=("replicas", "sharded", "pairs"), default="replicas",
                     help="replicas (every rank its own set, weak scaling; default), sharded (one set over "
                          "the ranks, strong scaling) or pairs (C4 genome pairs over the ranks)")
-    ap.add_argument("--pair-workers", type=int, default=12, help="pairs: pairs run at a time per GPU")
+    ap.add_argument("--pair-workers", type=int, default=16,
+                    help="pairs: pairs run at a time per GPU (16: the host cores a GPU is allotted; profiles/r04ka_pairs_worker_sweep.jsonl)")
     ap.add_argument("--pairs", type=int, default=0, help="pairs: the first P pairs only (0 = all)")
     ap.add_argument("--no-replicas-line", action="store_true",
                     help="N > 1: skip the secondary one-set (or, with --mode sharded, replica) measurement")

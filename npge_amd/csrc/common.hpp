@@ -299,8 +299,9 @@ hipStream_t aligner_stream(const npgx_aligner* al);
 const char* aligner_result(const npgx_aligner* al, const int64_t** row_off);
 std::string genome_of(const std::string& name);
 // a sequence set over text already on the device: sequence i is
-// [off[i], off[i+1]) of d_text and of host_text (ATGCN only, no names)
-npgx_seqset* seqset_from_device(const char* host_text, const char* d_text, const std::vector<int64_t>& off);
+// [off[i], off[i+1]) of d_text and of host_text (ATGCN only), named names[i]
+npgx_seqset* seqset_from_device(const char* host_text, const char* d_text, const std::vector<int64_t>& off,
+                                const std::vector<std::string>& names);
 void pack_device(npgx_seqset* s, const unsigned char* d_ascii, const std::vector<int64_t>& ascii);
 
 }  // namespace npgx

@@ -213,12 +213,14 @@ void pack_device(npgx_seqset* s, const unsigned char* d_ascii, const std::vector
     NPGX_HIP(hipDeviceSynchronize());
 }
 
-npgx_seqset* seqset_from_device(const char* host_text, const char* d_text, const std::vector<int64_t>& off) {
+npgx_seqset* seqset_from_device(const char* host_text, const char* d_text, const std::vector<int64_t>& off,
+                                const std::vector<std::string>& names) {
     const int32_t n = (int32_t)off.size() - 1;
+    NPGX_REQUIRE(names.size() == (size_t)n, NPGX_ERR_ARG, "one name per sequence");
     std::unique_ptr<npgx_seqset> s(new npgx_seqset);
     s->device = current_device_checked();
     s->n = n;
-    s->names.resize(n);
+    s->names = names;
     s->data.resize(n);
     heavy_for((size_t)n, off[n], [&](size_t i) { s->data[i].assign(host_text + off[i], (size_t)(off[i + 1] - off[i])); });
     pack_device(s.get(), (const unsigned char*)d_text, off);

@@ -1001,9 +1001,14 @@ struct BFrag {
     int64_t last() const { return ori == 1 ? max : min; }
 };
 
+// Block::Block() names a new block "00000000" (Block.cpp:29-34); ConSeq names
+// each consensus sequence after its block (Sequence.cpp:318-320), so the
+// consensus fragment ids -- and block_hash over them -- carry that name
+static const char* const NULL_BLOCK_NAME = "00000000";
+
 struct BBlock {
     std::vector<BFrag> f;
-    std::string name;
+    std::string name = NULL_BLOCK_NAME;
     int64_t aln_len() const {
         if (f.empty()) return 0;
         return f[0].has_row ? (int64_t)f[0].row.size() : f[0].length();

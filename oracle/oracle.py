@@ -455,6 +455,17 @@ def consensus_order(b):
     return sorted((f[0], f[1], f[2], f[3]) for f in b)
 
 
+# the name of a new Block (Block.cpp:29-34), which ConSeq gives every
+# consensus sequence of these pipes (Sequence.cpp:318-320)
+NULL_BLOCK_NAME = "00000000"
+
+
+def cons_names(cs):
+    """Names of the consensus sequences ConSeq makes: each block's name, the
+    null name for every block these pipes build."""
+    return [NULL_BLOCK_NAME] * len(cs)
+
+
 def anchor_loop_fast(o, workers=1):
     """AnchorLoopFast (src/algo/lua_lib.lua:741-758) over this restatement's
     processors, on BlockSetOracle `o` holding the current blocks:
@@ -471,10 +482,10 @@ def anchor_loop_fast(o, workers=1):
     o.apply("Rest")
     o.set_blocks(sorted(o.blocks(), key=consensus_order))
     cs = o.conseq()
-    oc = BlockSetOracle(cs, [""] * len(cs), portion_x1e4=5000, max_iterations=-1)
+    oc = BlockSetOracle(cs, cons_names(cs), portion_x1e4=5000, max_iterations=-1)
     if workers > 1:
         oc.set_workers(workers)
-    oc.set_blocks(anchor_blocks(AnchorFinder().run(cs, [""] * len(cs))))
+    oc.set_blocks(anchor_blocks(AnchorFinder().run(cs, cons_names(cs))))
     for op in ("DummyAligner", "FragmentsExtender", "Align"):
         oc.apply(op)
     it0 = oc.stats()["iterations"]

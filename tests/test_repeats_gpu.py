@@ -58,7 +58,7 @@ def test_repeat_anchor_groups_on_consensus():
     eng.apply("DraftPangenome", af=AnchorFinder())
     eng.apply("Filter").apply("Rest")
     cs = eng.conseq()
-    css = _capi.SeqSet(cs, [""] * len(cs))
+    css = _capi.SeqSet(cs, orc.cons_names(cs))
     af = AnchorFinder()
     r = af.find(css)
     bs = r["block_start"]

@@ -57,11 +57,11 @@ o.set_blocks(sorted(o.blocks(), key=consensus_order))
 ecs, ocs = eng.conseq(), o.conseq()
 print("ConSeq texts equal:", ecs == ocs, len(ecs), "sequences", flush=True)
 cs = ocs
-css = _capi.SeqSet(cs, [""] * len(cs))
+css = _capi.SeqSet(cs, orc.cons_names(cs))
 ce = BlockSetEngine(css, max_iterations=-1, extend_portion_x1e4=5000)
-oc = orc.BlockSetOracle(cs, [""] * len(cs), portion_x1e4=5000, max_iterations=-1)
+oc = orc.BlockSetOracle(cs, orc.cons_names(cs), portion_x1e4=5000, max_iterations=-1)
 ea = anchor_blocks(AnchorFinder().find(css))
-oa = oracle_anchor_blocks(orc.AnchorFinder().run(cs, [""] * len(cs)))
+oa = oracle_anchor_blocks(orc.AnchorFinder().run(cs, orc.cons_names(cs)))
 compare("consensus anchors", ea, oa)
 ce.set_blocks(oa)
 oc.set_blocks(oa)

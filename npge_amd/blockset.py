@@ -39,6 +39,9 @@ STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", 
 JOB_STATS = 24  # NPGX_JOB_STATS
 COUNTER_NAMES = ["blocks_after_extend", "filter_whole", "filter_slices", "blocks_after_filter",
                  "ou_in", "ou_rejected", "hashes", "spare"]
+# AnchorLoop's npgx_bb_stats.loop (the oracle's orc_bs_anchor_loop_stats, same order)
+ANCHOR_LOOP_NAMES = ["cons_seqs", "cons_anchors", "anchors_left", "split_blocks", "cons_blocks", "dec_blocks",
+                     "cons_iterations", "dec_iterations"]
 LOOP_NAMES = ["consensus_sequences", "anchors", "cons_blocks", "mapped_blocks", "loop_iterations",
               "unchanged_dropped"]
 LOOP_STAGE_NAMES = ["filter_rest", "conseq", "anchor_finder", "move_unchanged_dummy", "extend_and_align",
@@ -237,7 +240,12 @@ class BlockSetEngine:
         d["counters"] = {n: int(st.counters[i]) for i, n in enumerate(COUNTER_NAMES)}
         d["loop"] = {n: int(st.loop[i]) for i, n in enumerate(LOOP_NAMES)}
         d["ms_loop"] = {n: round(st.ms_loop[i], 3) for i, n in enumerate(LOOP_STAGE_NAMES)}
+        d["loop_raw"] = [int(x) for x in st.loop]  # per pipe: AnchorLoopFast's LOOP_NAMES or AnchorLoop's
         return d
+
+    def anchor_loop_stats(self):
+        """Counts of the last AnchorLoop (include/npge_amd.h, npgx_bb_stats.loop)."""
+        return dict(zip(ANCHOR_LOOP_NAMES, self.stats()["loop_raw"]))
 
     def job_stats(self):
         """(n_jobs, NPGX_JOB_STATS) int64 per alignment job of the last apply

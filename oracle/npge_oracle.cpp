@@ -2183,6 +2183,361 @@ static void draft_pangenome(std::vector<BSeq>& seqs, AnchorFinder& af, const Pip
     if (o.do_filter) filter_all(seqs, bs.blocks, o.filter, o.workers);
 }
 
+
+// ================================================================ AnchorLoop
+// The AnchorLoop pipe (lua_lib.lua:711-737) and the processors only it uses:
+// UniqueNames, RemoveWithSameName, SplitExtendable, ExtendLoop with
+// AddingLoopBySize.
+
+// block_less (block_hash.cpp:190-215): size, alignment length, the smallest
+// fragment (Fragment::operator<, the Sequence* compare pinned to the index)
+static bool block_less_ref(const BBlock& a, const BBlock& b) {
+    if (a.f.size() != b.f.size()) return a.f.size() < b.f.size();
+    if (a.f.empty()) return false;
+    if (a.aln_len() != b.aln_len()) return a.aln_len() < b.aln_len();
+    return frag_less(min_frag(a), min_frag(b));
+}
+
+// block_name (block_hash.cpp:132-177): u (one fragment), r (two fragments of
+// one genome), s (one per genome), h; then size "x" alignment length
+static std::string block_name(const std::vector<BSeq>& seqs, const BBlock& b, int genomes) {
+    bool repeats = false;
+    std::set<std::string> g;
+    for (const BFrag& f : b.f) {
+        if (!g.insert(seqs[(size_t)f.seq].genome).second) {
+            repeats = true;
+            break;
+        }
+    }
+    const char type = b.f.size() == 1 ? 'u' : repeats ? 'r' : (int)b.f.size() == genomes ? 's' : 'h';
+    return std::string(1, type) + std::to_string(b.f.size()) + "x" + std::to_string(b.aln_len());
+}
+
+// rand_name(8) (rand_name.cpp:34-46: 8 hex digits, a letter first) drawn from
+// the clock-seeded rand(); here the k-th name "a" + 7 hex digits of k
+static std::string det_seq_name(uint64_t k) {
+    static const char* const hex = "0123456789abcdef";
+    std::string r = "a0000000";
+    for (int i = 7; i >= 1; i--, k >>= 4) r[(size_t)i] = hex[k & 15];
+    return r;
+}
+
+// UniqueNames (UniqueNames.cpp:23-67): blocks with the null or an empty name
+// get their canonical name, then repeated names get "n1", "n2", ... in
+// block_greater order (ties: set order); sequences with an empty or a repeated
+// name get a fresh one
+static void unique_names(std::vector<BSeq>& seqs, std::vector<BBlock>& blocks) {
+    std::set<std::string> all_genomes;
+    for (const BSeq& s : seqs) all_genomes.insert(s.genome);
+    const int genomes = (int)all_genomes.size();
+    for (BBlock& b : blocks)
+        if (b.name == NULL_BLOCK_NAME || b.name.empty()) b.name = block_name(seqs, b, genomes);
+    std::vector<size_t> order(blocks.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](size_t a, size_t b) { return block_less_ref(blocks[b], blocks[a]); });
+    std::set<std::string> names;
+    std::map<std::string, int> last_n;
+    for (size_t i : order) {
+        BBlock& b = blocks[i];
+        if (names.count(b.name)) {
+            const std::string orig = b.name;
+            int& k = last_n[orig];
+            do {
+                k += 1;
+                b.name = orig + "n" + std::to_string(k);
+            } while (names.count(b.name));
+        }
+        names.insert(b.name);
+    }
+    std::set<std::string> snames;
+    uint64_t next = 0;
+    for (BSeq& s : seqs) {
+        while (s.name.empty() || snames.count(s.name)) s.name = det_seq_name(next++);
+        snames.insert(s.name);
+    }
+}
+
+// SplitExtendable::process_block_impl with find_extendable / try_extend
+// (SplitExtendable.cpp:46-84): the fragments of each block (std::set<Fragment*>,
+// pointer order; here block order) are taken off one by one; the first is
+// paired with each later one, the pair extended by FragmentsExtender::extend
+// (the child's defaults: extend-length MIN_LENGTH, portion 0) and cut by
+// Filter::find_good_subblocks; the first pair with good subblocks gives them
+// and loses its second fragment too
+static void split_extendable(const std::vector<BSeq>& seqs, const std::vector<BBlock>& blocks,
+                             const PipelineOpts& o, std::vector<BBlock>& out) {
+    for (const BBlock& blk : blocks) {
+        std::vector<BFrag> ff(blk.f.begin(), blk.f.end());
+        while (ff.size() >= 2) {
+            const BFrag a = ff[0];
+            ff.erase(ff.begin());
+            for (size_t j = 0; j < ff.size(); j++) {
+                BBlock pb;
+                pb.f.push_back(a);
+                pb.f.push_back(ff[j]);
+                fragments_extender(seqs, pb, o.extend_length, 0, o.im, nullptr);
+                std::vector<BBlock> gb;
+                filter_subblocks(seqs, pb, o.filter, gb);
+                if (!gb.empty()) {
+                    for (auto& x : gb) out.push_back(std::move(x));
+                    ff.erase(ff.begin() + (std::ptrdiff_t)j);
+                    break;
+                }
+            }
+        }
+    }
+}
+
+// SetFc::find_overlaps (FragmentCollection.hpp:319-364): the common part of f
+// with every fragment of the collection on f's sequence
+static void find_overlaps(const OverlapIndex& idx, const BFrag& f, std::vector<std::pair<int64_t, int64_t>>& out) {
+    out.clear();
+    auto it = idx.m.find(f.seq);
+    if (it == idx.m.end()) return;
+    for (const BFrag& g : it->second) {
+        const int64_t a = std::max(g.min, f.min), b = std::min(g.max, f.max);
+        if (a <= b) out.emplace_back(a, b);
+    }
+}
+
+// SmthUnion (TrySmth.cpp:35-155): `other`'s blocks by BlockLengthLess (size,
+// alignment length, name, all descending; std::sort ties pinned to
+// OverlaplessUnion's order) go to `target` when they overlap neither target
+// nor the subblocks made so far; a block overlapping a subblock becomes one;
+// a block overlapping only target is cut at the columns its overlaps cover
+// and its remaining column runs (Block::slice) become subblocks.  `other`
+// ends holding the subblocks.
+static void smth_union(const std::vector<BSeq>& seqs, std::vector<BBlock>& target, std::vector<BBlock>& other) {
+    OverlapIndex s2f, sub_idx;
+    for (const BBlock& b : target) s2f.add(b);
+    std::vector<size_t> order(other.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return ou_before(other[a], other[b]); });
+    std::vector<BBlock> subblocks;
+    std::vector<std::pair<int64_t, int64_t>> ovl;
+    for (size_t i : order) {
+        BBlock& b = other[i];
+        if (sub_idx.block_has_overlap(b)) {
+            sub_idx.add(b);
+            subblocks.push_back(std::move(b));
+        } else if (!s2f.block_has_overlap(b)) {
+            s2f.add(b);
+            target.push_back(std::move(b));
+        } else {
+            const int64_t L = b.aln_len();
+            std::vector<char> good((size_t)L, 1);
+            for (const BFrag& f : b.f) {
+                if (!f.has_row) throw std::logic_error("SmthUnion: block without alignment");
+                find_overlaps(s2f, f, ovl);
+                if (ovl.empty()) continue;
+                const RowMap rm(f.row);
+                for (const auto& ol : ovl) {
+                    // mark_bad (TrySmth.cpp:106-125): seq_to_frag, block_pos
+                    const int64_t fa = (ol.first - f.begin()) * f.ori, fb = (ol.second - f.begin()) * f.ori;
+                    const int64_t ba = rm.map_to_alignment(fa), bb = rm.map_to_alignment(fb);
+                    if (ba < 0 || bb < 0) throw std::logic_error("SmthUnion: overlap outside the row");
+                    for (int64_t c = std::min(ba, bb); c <= std::max(ba, bb); c++) good[(size_t)c] = 0;
+                }
+            }
+            // add_subblocks (TrySmth.cpp:127-147)
+            int64_t first = -1;
+            for (int64_t c = 0; c <= L; c++) {
+                const bool g = c < L && good[(size_t)c];
+                if (g && first == -1) first = c;
+                if (!g && first != -1) {
+                    BBlock sb = block_slice(seqs, b, first, c - 1);
+                    sub_idx.add(sb);
+                    subblocks.push_back(std::move(sb));
+                    first = -1;
+                }
+            }
+        }
+    }
+    other.swap(subblocks);
+}
+
+// AddingLoopBySize (TrySmth.cpp:157-178): while other has blocks, Align them
+// and SmthUnion them into target
+static void adding_loop_by_size(std::vector<BSeq>& seqs, std::vector<BBlock>& target, std::vector<BBlock>& other,
+                                const PipelineOpts& o) {
+    for (int guard = 0; !other.empty(); guard++) {
+        if (guard > 100000) throw std::logic_error("AddingLoopBySize does not converge");
+        BlockSetO t{&seqs, {}};
+        t.blocks.swap(other);
+        align_pipe(t, o, false);
+        other.swap(t.blocks);
+        smth_union(seqs, target, other);
+        static const bool dbg = getenv("ORACLE_AL_DEBUG") != nullptr;
+        if (dbg) fprintf(stderr, "  adding loop %d: target %zu other %zu\n", guard, target.size(), other.size());
+    }
+}
+
+// ExtendLoop (lua_lib.lua:677-688) under Pipe::run_impl (Pipe.cpp:60-78) with
+// set_max_iterations(-1): MoveUnchanged target=unchanged other=target;
+// ExtendAndAlign (FragmentsExtender --extend-length-portion:=0.5, Align);
+// Move target=target other=unchanged; AddingLoopBySize target=ol
+// other=target; Clear target; Move target=target other=ol; Clear ol
+static void extend_loop(BlockSetO& bs, const PipelineOpts& o, PipelineStats& st) {
+    std::vector<BSeq>& seqs = *bs.seqs;
+    std::set<uint64_t> seen_states;
+    seen_states.insert(blockset_hash(bs));
+    std::vector<uint64_t> mu_hashes;
+    for (int it = 0;; it++) {
+        if (it > 100000) throw std::logic_error("ExtendLoop does not converge");
+        st.iterations++;
+        std::vector<BBlock> unchanged;
+        BlockSetO work{&seqs, {}};
+        std::vector<uint64_t> fresh;
+        for (BBlock& b : bs.blocks) {
+            const uint64_t h = block_hash(seqs, b);
+            if (std::binary_search(mu_hashes.begin(), mu_hashes.end(), h)) unchanged.push_back(std::move(b));
+            else {
+                fresh.push_back(h);
+                work.blocks.push_back(std::move(b));
+            }
+        }
+        for (uint64_t h : fresh) mu_hashes.push_back(h);
+        std::sort(mu_hashes.begin(), mu_hashes.end());
+        mu_hashes.erase(std::unique(mu_hashes.begin(), mu_hashes.end()), mu_hashes.end());
+        for (BBlock& b : work.blocks)
+            fragments_extender(seqs, b, o.extend_length, 5000, o.im, &st.aligned_residues);
+        align_pipe(work, o, false);
+        for (BBlock& b : unchanged) work.blocks.push_back(std::move(b));
+        std::vector<BBlock> ol;
+        adding_loop_by_size(seqs, ol, work.blocks, o);
+        bs.blocks.swap(ol);
+        const uint64_t h = blockset_hash(bs);
+        static const bool dbg = getenv("ORACLE_AL_DEBUG") != nullptr;
+        if (dbg) fprintf(stderr, "extend_loop it %d: %zu blocks\n", it, bs.blocks.size());
+        if (seen_states.count(h)) break;
+        seen_states.insert(h);
+    }
+}
+
+// consensus_order: ConSeq's block order (the std::set<Block*> pointer order,
+// BlockSet.hpp:30) pinned to the blocks' sorted fragment coordinates
+static void consensus_sort(std::vector<BBlock>& blocks) {
+    auto key = [](const BBlock& b) {
+        std::vector<std::tuple<int, int64_t, int64_t, int>> k;
+        for (const BFrag& f : b.f) k.emplace_back(f.seq, f.min, f.max, f.ori);
+        std::sort(k.begin(), k.end());
+        return k;
+    };
+    std::vector<std::pair<std::vector<std::tuple<int, int64_t, int64_t, int>>, size_t>> ks(blocks.size());
+    for (size_t i = 0; i < blocks.size(); i++) ks[i] = {key(blocks[i]), i};
+    std::sort(ks.begin(), ks.end());
+    std::vector<BBlock> out;
+    out.reserve(blocks.size());
+    for (auto& k : ks) out.push_back(std::move(blocks[k.second]));
+    blocks.swap(out);
+}
+
+struct AnchorLoopStats {
+    int64_t cons_seqs = 0, cons_anchors = 0, anchors_left = 0, split_blocks = 0, cons_blocks = 0,
+            dec_blocks = 0, cons_iterations = 0, dec_iterations = 0;
+};
+
+// AnchorLoop (lua_lib.lua:711-737), a fresh pipe (its processors' memories
+// empty): Filter; Rest target=target other=target; ConSeq target=cons
+// other=target; AnchorFinder target=cons; MoveUnchanged target=null other=cons
+// (nothing seen yet); Clear null; DummyAligner target=cons; UniqueNames
+// target=cons; Union target=anchors other=cons; ExtendAndAlign target=cons;
+// RemoveWithSameName target=anchors other=cons; SplitExtendable other=anchors
+// target=cons; RemoveNames target=cons --remove-seqs-names:=0; DeConSeq
+// target=deconseq other=cons; ExtendLoop target=cons; ExtendLoop
+// target=deconseq; DeConSeq target=target other=cons; Align; Move
+// target=target other=deconseq; Clear cons, anchors, deconseq.
+static void anchor_loop(std::vector<BSeq>& seqs, BlockSetO& bs, const AnchorFinder& af_opts,
+                        const PipelineOpts& o, PipelineStats& st, AnchorLoopStats& al) {
+    static const bool dbg = getenv("ORACLE_AL_DEBUG") != nullptr;  // (diagnostic: phase sizes)
+    auto note = [&](const char* what, size_t n) {
+        if (dbg) fprintf(stderr, "anchor_loop %s: %zu\n", what, n);
+    };
+    filter_all(seqs, bs.blocks, o.filter, o.workers);
+    rest(seqs, bs.blocks);
+    consensus_sort(bs.blocks);
+    std::vector<BSeq> cseqs(bs.blocks.size());
+    std::vector<Seq> cin(bs.blocks.size());
+    for (size_t i = 0; i < bs.blocks.size(); i++) {
+        cseqs[i].name = bs.blocks[i].name;  // Sequence::set_block (Sequence.cpp:318-320)
+        cseqs[i].data = conseq_text(seqs, bs.blocks[i]);
+        cseqs[i].genome = genome_of(cseqs[i].name);
+        cseqs[i].index = (int)i;
+        cin[i].name = cseqs[i].name;
+        cin[i].data = cseqs[i].data;
+        cin[i].index = (int)i;
+    }
+    al.cons_seqs = (int64_t)cseqs.size();
+    BlockSetO cons{&cseqs, {}};
+    {
+        AnchorFinder caf;
+        caf.anchor = af_opts.anchor;
+        caf.fp_x1e4 = af_opts.fp_x1e4;
+        caf.similar = af_opts.similar;
+        caf.max_anchor_fragments = af_opts.max_anchor_fragments;
+        caf.seed = af_opts.seed;
+        caf.explicit_params = af_opts.explicit_params;
+        AnchorResult ar;
+        if (caf.run(cin, ar) != 0) throw std::logic_error("AnchorFinder on the consensus sequences failed");
+        for (size_t b = 0; b + 1 < ar.block_start.size(); b++) {
+            BBlock blk;
+            for (int64_t i = ar.block_start[b]; i < ar.block_start[b + 1]; i++) {
+                BFrag f;
+                f.seq = ar.frag_seq[(size_t)i];
+                f.min = ar.frag_min[(size_t)i];
+                f.max = ar.frag_max[(size_t)i];
+                f.ori = ar.frag_ori[(size_t)i];
+                blk.f.push_back(f);
+            }
+            cons.blocks.push_back(blk);
+        }
+    }
+    al.cons_anchors = (int64_t)cons.blocks.size();
+    for (BBlock& b : cons.blocks) align_block(cseqs, b, 1, o.im);  // DummyAligner
+    unique_names(cseqs, cons.blocks);
+    std::vector<BBlock> anchors = cons.blocks;  // Union (Block::clone keeps names and rows)
+    for (BBlock& b : cons.blocks) fragments_extender(cseqs, b, o.extend_length, 5000, o.im, &st.aligned_residues);
+    align_pipe(cons, o, false);
+    {  // RemoveWithSameName target=anchors other=cons (RemoveWithSameName.cpp:28-58)
+        std::set<std::string> names;
+        for (const BBlock& b : cons.blocks) names.insert(b.name);
+        std::vector<BBlock> keep;
+        for (BBlock& b : anchors)
+            if (!names.count(b.name)) keep.push_back(std::move(b));
+        anchors.swap(keep);
+    }
+    al.anchors_left = (int64_t)anchors.size();
+    note("anchors left", anchors.size());
+    {
+        std::vector<BBlock> gb;
+        split_extendable(cseqs, anchors, o, gb);
+        al.split_blocks = (int64_t)gb.size();
+        for (auto& x : gb) cons.blocks.push_back(std::move(x));
+    }
+    for (BBlock& b : cons.blocks) b.name.clear();  // RemoveNames --remove-seqs-names:=0 (RemoveNames.cpp:26-35)
+    BlockSetO dec{&seqs, {}};
+    for (const BBlock& cb : cons.blocks) dec.blocks.push_back(deconseq_block(seqs, bs.blocks, cb));
+    PipelineStats sc, sd;
+    note("split done, cons blocks", cons.blocks.size());
+    extend_loop(cons, o, sc);
+    note("cons ExtendLoop done", cons.blocks.size());
+    extend_loop(dec, o, sd);
+    note("deconseq ExtendLoop done", dec.blocks.size());
+    st.aligned_residues += sc.aligned_residues + sd.aligned_residues;
+    al.cons_iterations = sc.iterations;
+    al.dec_iterations = sd.iterations;
+    al.cons_blocks = (int64_t)cons.blocks.size();
+    al.dec_blocks = (int64_t)dec.blocks.size();
+    {
+        std::vector<BBlock> add;
+        for (const BBlock& cb : cons.blocks) add.push_back(deconseq_block(seqs, bs.blocks, cb));
+        for (auto& b : add) bs.blocks.push_back(std::move(b));
+    }
+    align_pipe(bs, o, false);
+    for (auto& b : dec.blocks) bs.blocks.push_back(std::move(b));
+}
+
 }  // namespace orc
 
 // ============================================================================
@@ -2329,6 +2684,7 @@ struct orc_bs {
     orc::PipelineStats st;
     orc::AnchorFinder af;
     orc::PipelineOpts po;
+    orc::AnchorLoopStats al;
 };
 
 // params (int64): [0] extend_length, [1] portion_x1e4, [2] fix_min_fragment,
@@ -2408,7 +2764,9 @@ void orc_bs_set_workers(orc_bs* h, int workers) { h->af.workers = h->po.workers 
 // 5 RemoveNonStem --exact, 6 DraftPangenome (AnchorFinder on all sequences first),
 // 7 MetaAligner(similar) align_block, 8 Filter::find_good_subblocks, 9 Rest,
 // 10 OverlaplessUnion --ou-move, 11 MoveGaps, 12 CutGaps, 13 CutGaps --cut-strict,
-// 14 SelfOverlapsResolver, 15 Align, 16 LiteAlign
+// 14 SelfOverlapsResolver, 15 Align, 16 LiteAlign, 17 AnchorLoop (a fresh pipe;
+// its consensus AnchorFinder takes this set's AnchorFinder options),
+// 18 ExtendLoop, 19 AddingLoopBySize into an empty target
 static int bs_apply(orc_bs* h, int op);
 // op codes: see bs_apply; exceptions (the reference's ASSERTs) -> -2
 int orc_bs_apply(orc_bs* h, int op) {
@@ -2487,6 +2845,19 @@ static int bs_apply(orc_bs* h, int op) {
         case 16:
             orc::align_pipe(h->bs, o, op == 16);
             return 0;
+        case 17:
+            h->al = orc::AnchorLoopStats{};
+            orc::anchor_loop(h->seqs, h->bs, h->af, o, h->st, h->al);
+            return 0;
+        case 18:
+            orc::extend_loop(h->bs, o, h->st);
+            return 0;
+        case 19: {
+            std::vector<orc::BBlock> target;
+            orc::adding_loop_by_size(h->seqs, target, h->bs.blocks, o);
+            h->bs.blocks.swap(target);
+            return 0;
+        }
     }
     return -1;
 }
@@ -2535,6 +2906,16 @@ void orc_bs_copy(const orc_bs* h, int64_t* block_start, int32_t* seq, int64_t* m
 }
 
 uint64_t orc_bs_hash(const orc_bs* h) { return orc::blockset_hash(h->bs); }
+
+// the last AnchorLoop's counts: [consensus sequences, consensus anchor blocks,
+// anchors left for SplitExtendable, its blocks, consensus blocks after
+// ExtendLoop, deconseq blocks after ExtendLoop, the two ExtendLoop iterations]
+void orc_bs_anchor_loop_stats(const orc_bs* h, int64_t* c) {
+    const orc::AnchorLoopStats& a = h->al;
+    const int64_t v[8] = {a.cons_seqs, a.cons_anchors, a.anchors_left, a.split_blocks,
+                          a.cons_blocks, a.dec_blocks, a.cons_iterations, a.dec_iterations};
+    memcpy(c, v, sizeof(v));
+}
 
 // goodSlices (goodSlices.cpp:247-255) over n column scores: the slices'
 // (start, stop) pairs into out (at most max_out); returns their count

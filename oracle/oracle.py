@@ -300,7 +300,8 @@ _PKEYS = list(PIPELINE_DEFAULTS)
 OPS = {"FragmentsExtender": 0, "FixEnds": 1, "Filter": 2, "ExtendLoopFast": 3, "DummyAligner": 4,
        "RemoveNonStem": 5, "DraftPangenome": 6, "MetaAligner": 7, "FindGoodSubblocks": 8,
        "Rest": 9, "OverlaplessUnion": 10, "MoveGaps": 11, "CutGaps": 12, "CutGapsStrict": 13,
-       "SelfOverlapsResolver": 14, "Align": 15, "LiteAlign": 16}
+       "SelfOverlapsResolver": 14, "Align": 15, "LiteAlign": 16, "AnchorLoop": 17, "ExtendLoop": 18,
+       "AddingLoopBySize": 19}
 
 
 def _bs_lib():
@@ -323,6 +324,7 @@ def _bs_lib():
         L.orc_bs_deconseq.argtypes = [vp, vp, vp]
         L.orc_bs_deconseq.restype = ctypes.c_int
         L.orc_bs_set_gap_opts.argtypes = [vp, ctypes.c_int, i64]
+        L.orc_bs_anchor_loop_stats.argtypes = [vp, vp]
         L._bs_bound = True
     return L
 
@@ -331,8 +333,8 @@ class BlockSetOracle:
     """Oracle block set: sequences + blocks, with the hot-path processors
     (FragmentsExtender, FixEnds, Filter, ExtendLoopFast, DummyAligner,
     RemoveNonStem, DraftPangenome, MetaAligner, Rest, OverlaplessUnion,
-    MoveGaps, CutGaps (permissive / strict), SelfOverlapsResolver and the
-    Align / LiteAlign pipes)."""
+    MoveGaps, CutGaps (permissive / strict), SelfOverlapsResolver, the
+    Align / LiteAlign pipes, ExtendLoop, AddingLoopBySize and AnchorLoop)."""
 
     def __init__(self, seqs, names, max_tail=3, max_tail_to_gap_x1e4=10000, **params):
         L = _bs_lib()
@@ -417,6 +419,14 @@ class BlockSetOracle:
 
     def hash(self):
         return _bs_lib().orc_bs_hash(self._h)
+
+    def anchor_loop_stats(self):
+        """Counts of the last AnchorLoop (orc_bs_anchor_loop_stats)."""
+        c = np.zeros(8, dtype=np.int64)
+        _bs_lib().orc_bs_anchor_loop_stats(self._h, _ptr(c))
+        keys = ("cons_seqs", "cons_anchors", "anchors_left", "split_blocks", "cons_blocks", "dec_blocks",
+                "cons_iterations", "dec_iterations")
+        return dict(zip(keys, (int(x) for x in c)))
 
     def conseq(self):
         """ConSeq (ConSeq.cpp:37-50): the sequence text each block becomes."""

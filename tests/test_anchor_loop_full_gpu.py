@@ -1,0 +1,70 @@
+"""The AnchorLoop pipe (lua_lib.lua:711-737) and the processors only it uses
+-- UniqueNames, RemoveWithSameName, SplitExtendable (SplitExtendable.cpp:46-84),
+ExtendLoop (lua_lib.lua:677-688) with AddingLoopBySize / SmthUnion
+(TrySmth.cpp:35-178) -- on the engine vs the oracle's restatement
+(oracle/npge_oracle.cpp anchor_loop): fragments and rows bit-exact, the
+pipe's counts equal.  Parity is pinned to the restatement (the reference
+has no fixture for these pipes) and to its conventions."""
+import pytest
+
+from oracle import oracle as orc
+from npge_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def canon(blocks):
+    return sorted(tuple(sorted(b)) for b in blocks)
+
+
+def _engine(seqs, names, blocks):
+    from npge_amd import _capi
+    from npge_amd.blockset import BlockSetEngine
+    return BlockSetEngine(_capi.SeqSet(seqs, names)).set_blocks(blocks)
+
+
+@pytest.mark.parametrize("cfg", ["tiny", "rtiny", "small"])
+def test_anchor_loop(cfg):
+    from npge_amd.anchor_finder import AnchorFinder
+    names, seqs = synth.genome_set(cfg)
+    o = orc.BlockSetOracle(seqs, names)
+    o.apply("DraftPangenome")
+    start = o.blocks()
+    eng = _engine(seqs, names, start)
+    eng.apply("AnchorLoop", af=AnchorFinder())
+    o.set_blocks(start)
+    o.apply("AnchorLoop")
+    est, ost = eng.anchor_loop_stats(), o.anchor_loop_stats()
+    assert est == ost
+    assert ost["anchors_left"] > 0 and ost["split_blocks"] > 0
+    assert canon(eng.blocks()) == canon(o.blocks())
+
+
+def test_extend_loop():
+    """ExtendLoop alone, from DummyAligner'd anchors."""
+    from npge_amd.anchor_loop import anchor_blocks
+    names, seqs = synth.genome_set("tiny")
+    o = orc.BlockSetOracle(seqs, names)
+    o.set_blocks(anchor_blocks(orc.AnchorFinder().run(seqs, names)))
+    o.apply("DummyAligner")
+    start = o.blocks()
+    eng = _engine(seqs, names, start)
+    eng.apply("ExtendLoop")
+    o.apply("ExtendLoop")
+    assert len(o.blocks()) > 0
+    assert eng.stats()["iterations"] == o.stats()["iterations"]
+    assert canon(eng.blocks()) == canon(o.blocks())
+
+
+def test_adding_loop_by_size():
+    """AddingLoopBySize alone on overlapping blocks (DraftPangenome's and
+    their 50-bp shifted copies): the cuts of SmthUnion, bit-exact."""
+    from test_oracle_anchor_loop import overlapping_input, overlaps
+    names, seqs, blocks = overlapping_input()
+    eng = _engine(seqs, names, blocks)
+    eng.apply("AddingLoopBySize")
+    o = orc.BlockSetOracle(seqs, names)
+    o.set_blocks(blocks)
+    o.apply("AddingLoopBySize")
+    assert overlaps(o.blocks()) == 0
+    assert canon(eng.blocks()) == canon(o.blocks())

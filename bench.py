@@ -56,8 +56,9 @@ def parse():
     ap.add_argument("--pairs-config", default="C4", help="the secondary pairs line's config")
     ap.add_argument("--no-pairs-line", action="store_true",
                     help="skip the secondary C4 pair-sharded measurement")
-    ap.add_argument("--anchor-loop", action="store_true",
-                    help="each step also runs one AnchorLoopFast after DraftPangenome (lua_lib.lua:741-758)")
+    ap.add_argument("--anchor-loop", nargs="?", const="fast", default=False, choices=["fast", "full"],
+                    help="each step also runs one AnchorLoopFast (fast, lua_lib.lua:741-758) or one AnchorLoop "
+                         "(full, lua_lib.lua:711-737) after DraftPangenome")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one rank per GPU) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -265,7 +266,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample or args.config, args.cpu_runs)
         if args.anchor_loop:  # the CPU leg times DraftPangenome only: not like-for-like
-            cpu["workload"] = "DraftPangenome only (the GPU step adds AnchorLoopFast): no speedup ratio implied"
+            cpu["workload"] = ("DraftPangenome only (the GPU step adds %s): no speedup ratio implied"
+                               % ("AnchorLoop" if args.anchor_loop == "full" else "AnchorLoopFast"))
 
     if rank == 0:
         line = {

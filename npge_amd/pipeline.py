@@ -1,9 +1,10 @@
 """Block-build driver used by bench.py and smoke(): one step = DraftPangenome on
 a device-resident genome set (AnchorFinder -> RemoveNonStem --exact ->
 DummyAligner -> ExtendLoopFast(10) -> Filter, src/algo/lua_lib.lua:1569-1621),
-optionally followed by one AnchorLoopFast (lua_lib.lua:741-758), the pipe the
-real pipeline grows blocks with where the exact stem anchors are too few
-(C4: 32 genomes at 2 % divergence).
+optionally followed by one AnchorLoopFast (lua_lib.lua:741-758) or one
+AnchorLoop (lua_lib.lua:711-737), the pipes the real pipeline grows blocks
+with where the exact stem anchors are too few (C4: 32 genomes at 2 %
+divergence).
 """
 from .anchor_finder import AnchorFinder
 from .blockset import BlockSetEngine
@@ -15,8 +16,10 @@ class BlockBuild:
     def __init__(self, seqset, names, seqs, seed=1, comm=None, anchor_loop=False, lender=None):
         self.ss = seqset
         self.seed = seed
-        self.anchor_loop = anchor_loop
-        self.loop_af = AnchorFinder() if anchor_loop else None
+        # anchor_loop: False, True / "fast" (AnchorLoopFast) or "full" (AnchorLoop)
+        self.loop_pipe = {True: "AnchorLoopFast", "fast": "AnchorLoopFast", "full": "AnchorLoop"}.get(anchor_loop)
+        self.anchor_loop = self.loop_pipe is not None
+        self.loop_af = AnchorFinder() if self.anchor_loop else None
         # lender: a BlockBuild whose aligner this one borrows (never run together)
         self.eng = BlockSetEngine(seqset, lender=lender.eng if lender is not None else None)
         if comm is not None:  # one genome set sharded over the ranks of comm
@@ -28,7 +31,7 @@ class BlockBuild:
 
     def workload_name(self, config):
         return "%s DraftPangenome: %s%s" % (config, " -> ".join(STAGES),
-                                            " -> AnchorLoopFast" if self.anchor_loop else "")
+                                            " -> " + self.loop_pipe if self.anchor_loop else "")
 
     def run(self):
         # one AnchorFinder handle (device buffers kept); its used-hash set is
@@ -41,10 +44,11 @@ class BlockBuild:
             draft_kt = self.eng.kernel_times()
             self.loop_af.clear_used()
             self.eng.reset_loop()
-            self.eng.apply("AnchorLoopFast", af=self.loop_af)
+            self.eng.apply(self.loop_pipe, af=self.loop_af)
             lst = self.eng.stats()
-            loop = dict(lst["loop"], ms_host=round(lst["ms_host"], 3), ms_align=round(lst["ms_align"], 3),
-                        ms_loop=lst["ms_loop"], ms_stage=lst["ms_stage"])
+            counts = lst["loop"] if self.loop_pipe == "AnchorLoopFast" else self.eng.anchor_loop_stats()
+            loop = dict(counts, pipe=self.loop_pipe, ms_host=round(lst["ms_host"], 3),
+                        ms_align=round(lst["ms_align"], 3), ms_loop=lst["ms_loop"], ms_stage=lst["ms_stage"])
             self._extra_kt = draft_kt + self.loop_af.kernel_times()
         else:
             self._extra_kt = []

@@ -277,6 +277,16 @@ int npgx_refine_batch(const char* rows, const int64_t* row_off, const int32_t* j
  *                        (src/algo/OverlaplessUnion.cpp:54-80)
  *   "AnchorLoopFast"     the AnchorLoopFast pipe (lua_lib.lua:741-758), af =
  *                        its AnchorFinder
+ *   "AnchorLoop"         the AnchorLoop pipe (lua_lib.lua:711-737) as a fresh
+ *                        pipe, af = its AnchorFinder: ConSeq, AnchorFinder,
+ *                        DummyAligner, UniqueNames (UniqueNames.cpp:23-67),
+ *                        ExtendAndAlign, RemoveWithSameName
+ *                        (RemoveWithSameName.cpp:28-58), SplitExtendable
+ *                        (SplitExtendable.cpp:46-84), RemoveNames, DeConSeq,
+ *                        ExtendLoop on both sets, DeConSeq, Align
+ *   "ExtendLoop"         Pipe ExtendLoop (lua_lib.lua:677-688) to its fixpoint
+ *   "AddingLoopBySize"   AddingLoopBySize (src/algo/TrySmth.cpp:157-178) of all
+ *                        blocks into an empty target (SmthUnion, :35-155)
  *   "FragmentsExtender"  FragmentsExtender (src/algo/FragmentsExtender.cpp:87-119)
  *   "FixEnds"            FixEnds (src/algo/FixEnds.cpp:117-144)
  *   "ExtendLoopFast"     Pipe ExtendLoopFast (src/algo/lua_lib.lua:697-709,
@@ -327,7 +337,10 @@ typedef struct {
     /* AnchorLoopFast: 0 consensus sequences, 1 anchor blocks on them, 2
      * consensus blocks after the pipe's ExtendLoopFast, 3 blocks DeConSeq
      * added, 4 the consensus ExtendLoopFast's iterations, 5 consensus blocks
-     * MoveUnchanged dropped */
+     * MoveUnchanged dropped.  AnchorLoop: 0 consensus sequences, 1 anchor
+     * blocks on them, 2 anchors left for SplitExtendable, 3 its blocks, 4
+     * consensus blocks after ExtendLoop, 5 deconseq blocks after ExtendLoop,
+     * 6 / 7 the two ExtendLoop's iterations */
     int64_t loop[8];
     /* AnchorLoopFast wall ms: 0 Filter + Rest + order, 1 ConSeq, 2 AnchorFinder
      * on the consensus sequences, 3 MoveUnchanged + DummyAligner, 4

@@ -178,6 +178,37 @@ class OverlaplessUnion(_EngineProcessor):
 
 
 @register
+class ExtendLoop(_EngineProcessor):
+    """The ExtendLoop pipe (lua_lib.lua:677-688) to its fixpoint: MoveUnchanged,
+    ExtendAndAlign, AddingLoopBySize, until the block set repeats."""
+    name = "ExtendLoop"
+    engine_name = "ExtendLoop"
+
+
+@register
+class AddingLoopBySize(_EngineProcessor):
+    """AddingLoopBySize (TrySmth.cpp:157-178): Align other's blocks and move
+    the overlapless ones (cut where they overlap) into target, until other is
+    empty.  The engine starts from an empty target, so target must be empty
+    here; other ends empty."""
+    name = "AddingLoopBySize"
+    engine_name = "AddingLoopBySize"
+
+    def run_impl(self):
+        t, o = self.block_set(), self.other()
+        if t is o:
+            super().run_impl()
+            return
+        if t.blocks:
+            raise OptionError("AddingLoopBySize: the fixed-form runner needs an empty target")
+        for sq in o.seqs:
+            if all(sq is not x for x in t.seqs):
+                t.seqs.append(sq)
+        t.blocks, o.blocks = o.blocks, []
+        super().run_impl()
+
+
+@register
 class RemoveAlignment(Processor):
     """RemoveAlignment: every fragment loses its row."""
     name = "RemoveAlignment"

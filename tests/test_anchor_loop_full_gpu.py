@@ -23,8 +23,9 @@ def _engine(seqs, names, blocks):
     return BlockSetEngine(_capi.SeqSet(seqs, names)).set_blocks(blocks)
 
 
-@pytest.mark.parametrize("cfg", ["tiny", "rtiny", "small"])
+@pytest.mark.parametrize("cfg", ["tiny", "rtiny", "small", "C2"])
 def test_anchor_loop(cfg):
+    """C2 (3 genomes, 9.9 Mbp): the oracle pipe takes about 90 s on one thread."""
     from npge_amd.anchor_finder import AnchorFinder
     names, seqs = synth.genome_set(cfg)
     o = orc.BlockSetOracle(seqs, names)

@@ -2,7 +2,8 @@
 """Host-side sampling profile of the block build (diagnostic; GPU box):
 SIGPROF sampling inside libnpge_amd.so (npge_amd/csrc/host_sampler.cpp)
 during a few DraftPangenome steps; prints the hottest library functions.
-usage: host_profile.py [config] [steps] [alf]  (alf: DraftPangenome -> AnchorLoopFast)"""
+usage: host_profile.py [config] [steps] [alf|full]  (alf: DraftPangenome ->
+AnchorLoopFast; full: DraftPangenome -> AnchorLoop)"""
 import collections
 import ctypes
 import os
@@ -24,7 +25,8 @@ if cfg.endswith(":pair"):  # the first genome pair of a config (the pair-sharded
 else:
     names, seqs = synth.genome_set(cfg)
 ss = _capi.SeqSet(seqs, names)
-job = pipeline.BlockBuild(ss, names, seqs, anchor_loop=len(sys.argv) > 3 and sys.argv[3] == "alf")
+loop = sys.argv[3] if len(sys.argv) > 3 else ""
+job = pipeline.BlockBuild(ss, names, seqs, anchor_loop={"alf": "fast", "full": "full"}.get(loop, False))
 job.run()
 out = os.path.abspath("gpurun_out/host_prof_%s.txt" % cfg.replace(":", "_"))
 os.makedirs(os.path.dirname(out), exist_ok=True)

@@ -20,4 +20,9 @@ for cfg in CFGS:
             af.clear_used()
             t = time.perf_counter(); af.find(ss); dt = time.perf_counter() - t
             best = min(best, dt)
-        print(cfg, "epochs", ep, "af %.2f ms" % (best * 1e3), flush=True)
+        agg = {}
+        for k in af.kernel_times():  # the last run's kernels (NPGX_TIMERS=2: all of them)
+            agg[k["name"]] = agg.get(k["name"], 0.0) + k["ms"]
+        top = sorted(agg.items(), key=lambda kv: -kv[1])[:5]
+        print(cfg, "epochs", ep, "af %.2f ms" % (best * 1e3),
+              " ".join("%s %.2f" % (n, v) for n, v in top), flush=True)

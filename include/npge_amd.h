@@ -340,7 +340,10 @@ typedef struct {
      * MoveUnchanged dropped.  AnchorLoop: 0 consensus sequences, 1 anchor
      * blocks on them, 2 anchors left for SplitExtendable, 3 its blocks, 4
      * consensus blocks after ExtendLoop, 5 deconseq blocks after ExtendLoop,
-     * 6 / 7 the two ExtendLoop's iterations */
+     * 6 / 7 the two ExtendLoop's iterations (AnchorLoop: counters[7] =
+     * AddingLoopBySize rounds, ms_loop = 0 Filter..AnchorFinder, 1
+     * DummyAligner..RemoveWithSameName, 2 SplitExtendable, 3 DeConSeq, 4 / 5
+     * the two ExtendLoops, 6 DeConSeq, 7 Align) */
     int64_t loop[8];
     /* AnchorLoopFast wall ms: 0 Filter + Rest + order, 1 ConSeq, 2 AnchorFinder
      * on the consensus sequences, 3 MoveUnchanged + DummyAligner, 4

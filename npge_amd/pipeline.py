@@ -46,7 +46,14 @@ class BlockBuild:
             self.eng.reset_loop()
             self.eng.apply(self.loop_pipe, af=self.loop_af)
             lst = self.eng.stats()
-            counts = lst["loop"] if self.loop_pipe == "AnchorLoopFast" else self.eng.anchor_loop_stats()
+            if self.loop_pipe == "AnchorLoopFast":
+                counts = lst["loop"]
+            else:
+                counts = dict(self.eng.anchor_loop_stats(), adding_loop_rounds=lst["counters"]["spare"])
+                lst["ms_loop"] = dict(zip(["filter_to_anchor_finder", "dummy_to_remove_with_same_name",
+                                           "split_extendable", "deconseq_1", "extend_loop_cons",
+                                           "extend_loop_deconseq", "deconseq_2", "align"],
+                                          lst["ms_loop"].values()))
             loop = dict(counts, pipe=self.loop_pipe, ms_host=round(lst["ms_host"], 3),
                         ms_align=round(lst["ms_align"], 3), ms_loop=lst["ms_loop"], ms_stage=lst["ms_stage"])
             self._extra_kt = draft_kt + self.loop_af.kernel_times()

@@ -69,3 +69,28 @@ def test_adding_loop_by_size():
     o.apply("AddingLoopBySize")
     assert overlaps(o.blocks()) == 0
     assert canon(eng.blocks()) == canon(o.blocks())
+
+
+def test_processor_mirror():
+    """new_p('AddingLoopBySize') / new_p('ExtendLoop') of the Python mirror
+    (lua_lib.lua:59-61 call shapes) over model block sets: the engine's
+    blocks, through the same C ABI."""
+    from test_oracle_anchor_loop import overlapping_input
+    from npge_amd import script  # noqa: F401  (registers the engine processors)
+    from npge_amd.model import Block, BlockSet, Fragment, Sequence
+    from npge_amd.processor import new_p
+    names, seqs, blocks = overlapping_input()
+    sq = [Sequence(n, s) for n, s in zip(names, seqs)]
+    other = BlockSet(seqs=list(sq), blocks=[Block([Fragment(sq[f[0]], f[1], f[2], f[3], f[4]) for f in b])
+                                            for b in blocks])
+    target = BlockSet(seqs=list(sq))
+    p = new_p("AddingLoopBySize")
+    p.set_bs("target", target)
+    p.set_bs("other", other)
+    p.run()
+    got = canon([[(sq.index(f.seq), f.min_pos, f.max_pos, f.ori, f.row) for f in b.fragments]
+                 for b in target.blocks])
+    o = orc.BlockSetOracle(seqs, names)
+    o.set_blocks(blocks)
+    o.apply("AddingLoopBySize")
+    assert not other.blocks and got == canon(o.blocks())

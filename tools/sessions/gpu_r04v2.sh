@@ -6,6 +6,10 @@ set -o pipefail
 R=$(pwd)
 TAG=${1:-r04v}
 O=$R/gpurun_out/$TAG
+mkdir -p $O
+echo "== pytest anchor loop $(date +%T)"
+timeout -k 10 900 python -u -m pytest tests/test_anchor_loop_full_gpu.py -m gpu -x -q --timeout 500 --timeout-method thread > $O/pytest_al.log 2>&1 || { tail -40 $O/pytest_al.log | cut -c1-300; exit 1; }
+tail -1 $O/pytest_al.log
 tools/round_end.sh $TAG perf || exit 1
 for cfg in C2 C3; do
   echo "== bench $cfg AnchorLoop $(date +%T)"

@@ -445,9 +445,13 @@ def pmc_traffic(kernel, config):
     tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
     of this bench).  PMC counters cannot be read from inside this process."""
     import glob
-    # newest session tag: r03z < r03aa < r03ab (shorter tags first)
+    # newest session tag: by round, then r03z < r03aa < r03ab (shorter suffixes first)
+    def tag_key(f):
+        tag = os.path.basename(f).split("_")[0]
+        rnd = int(tag[1:3]) if tag[1:3].isdigit() else 0
+        return (rnd, len(tag[3:]), tag[3:])
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_%s_pmc_traffic.json" % config.lower())),
-                   key=lambda f: (len(os.path.basename(f).split("_")[0]), os.path.basename(f)))
+                   key=tag_key)
     if not files:
         return {"traffic": None}
     doc = json.load(open(files[-1]))

@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default=None, help="synthetic config timed for cpu_baseline (default: --config)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU runs (median) after one warm-up")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="hardware queues per process (GPU_MAX_HW_QUEUES; HIP's default is 4): the pair job runs "
+                         "--pair-workers streams at once (16 queues: +5 %%, profiles/r04ab_ab_hw_queues.txt); "
+                         "0 leaves the environment alone")
     ap.add_argument("--launch-check", action="store_true",
                     help="only the rank launch and rendezvous (no GPU call): prints n_gpus and the "
                          "communicator's rank count (tests/test_bench_launch.py)")
@@ -132,6 +136,8 @@ def launch_check(args, world, rank):
 
 def main():
     args = parse()
+    if args.hw_queues > 0:  # read by the HIP runtime when it starts: before any GPU call (ranks inherit it)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))  # nothing here has touched the GPU
     world, rank, local_rank = ranks_from_env(args)

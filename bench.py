@@ -64,10 +64,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default=None, help="synthetic config timed for cpu_baseline (default: --config)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU runs (median) after one warm-up")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--hw-queues", type=int, default=20,
                     help="hardware queues per process (GPU_MAX_HW_QUEUES; HIP's default is 4): the pair job runs "
-                         "--pair-workers streams at once (16 queues: +5 %%, profiles/r04ab_ab_hw_queues.txt); "
-                         "0 leaves the environment alone")
+                         "--pair-workers streams at once; 20 queues with 16 workers: +9 %%, 24 or more: far slower "
+                         "(profiles/r04ab_ab_hw_queues.txt, r04ac_pairs_workers_queues_*.jsonl); 0 leaves the "
+                         "environment alone")
     ap.add_argument("--launch-check", action="store_true",
                     help="only the rank launch and rendezvous (no GPU call): prints n_gpus and the "
                          "communicator's rank count (tests/test_bench_launch.py)")

@@ -72,3 +72,23 @@ def test_repeat_anchor_groups_on_consensus():
             t = cs[q][mn:mx + 1]
             texts.add(t if ori == 1 else t.translate(comp)[::-1])
         assert len(texts) == 1 and bs[b + 1] - bs[b] >= 2
+
+
+def test_r3_draft_fullsize():
+    """R3 (C3-shaped: 17 genomes, 56 Mbp, with the element families and
+    inversions): DraftPangenome bit-exact at full size, rows by digest --
+    the set whose aligner share is 7x C3's (Measurement)."""
+    from helpers import rows_digest
+    from npge_amd import _capi
+    from npge_amd.anchor_finder import AnchorFinder
+    from npge_amd.blockset import BlockSetEngine
+    names, seqs = synth.genome_set("R3")
+    eng = BlockSetEngine(_capi.SeqSet(seqs, names))
+    eng.apply("DraftPangenome", af=AnchorFinder())
+    o = orc.BlockSetOracle(seqs, names)
+    o.set_workers(8)  # BlocksJobs threads: output identical for any count
+    o.apply("DraftPangenome")
+    ob = o.blocks()
+    assert len(ob) > 1000
+    assert canon([[f[:4] for f in b] for b in eng.blocks()]) == canon([[f[:4] for f in b] for b in ob])
+    assert eng.rows_digest() == rows_digest(ob)

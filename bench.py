@@ -265,9 +265,9 @@ def main():
         pairs_line = run_pairs(args, dist, world, rank, local_rank, comm, args.pairs_config, args.pairs,
                                min(args.steps, 2), 1, baseline=not args.no_cpu_baseline, cpu_runs=3)
         if pairs_line is not None:
-            pairs_line = {k: pairs_line[k] for k in ("value", "unit", "ms_per_step", "scaling", "config",
-                                                     "last_step", "device_mem_used_gb", "roofline",
-                                                     "cpu_baseline")}
+            pairs_line = {k: pairs_line[k] for k in ("value", "unit", "unit_note", "input_set_mbp_s",
+                                                     "ms_per_step", "scaling", "config", "last_step",
+                                                     "device_mem_used_gb", "roofline", "cpu_baseline")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

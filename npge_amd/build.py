@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "libnpge_amd.so")
 LIB_PROF = os.path.join(HERE, "libnpge_amd_prof.so")
 SOURCES = ["seqset.hip", "anchor_finder.hip", "similar_aligner.hip", "block_build.hip",
            "general_aligner.hip", "wide_aligner.hip", "comm_rccl.hip", "host_sampler.cpp"]
-HEADERS = ["common.hpp", "sa_device.hpp", "log_score.inc"]
+HEADERS = ["common.hpp", "sa_device.hpp", "log_score.inc", "elf_device.inc"]
 ARCH = os.environ.get("NPGX_OFFLOAD_ARCH", "gfx950")
 
 

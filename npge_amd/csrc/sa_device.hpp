@@ -44,6 +44,8 @@ struct View {
 struct Params {
     int mc, gc, ac, min_length;
     int wf;  // FindLowSimilar weight factor (FindLowSimilar.cpp:56-60)
+    int lh;  // try_aligned: shifts searched incrementally before the prefix search (0: never switch)
+    int lm;  // ... the prefix search's first prefix (shifts)
 };
 
 // Per-wave scratch (global memory), sized by the host for the batch.
@@ -482,6 +484,256 @@ __device__ __noinline__ VecOut find_word_vec(const char* vp, int vlen, int vd, i
     return out;
 }
 
+// ------------------------------------------------------------ long word searches
+// try_aligned (:295-308) when the first complete word lies far away (rows
+// unrelated over hundreds or thousands of bases: inversions, insertions).
+// The incremental searches above take the shifts one after the other, each
+// paying a round of word-table atomics (a shift cost ~2800 cycles on the
+// repeat-rich R3 set).  Past their first shifts this search answers the
+// same question for a whole prefix of shifts [0, M) and doubles M until the
+// answer lies inside:
+//   T(w)  = max over rows k of first_k(w): the shift at which the reference's
+//           ff[w] becomes complete (every row has sighted w);
+//   S*    = min over w of T(w): the shift at which try_aligned stops;
+//   best  = word_i(S*) of the highest row i whose word is complete at S*
+//           (find_best_word overwrites best_word row by row);
+//   shift = first_k(best) per row, or S* for every row when all rows hold
+//           the same word at S* (words.size() == 1).
+// A complete word is one of row 0's words, so the table holds row 0's words
+// of [0, M) only (at most M keys, not n x M), each with a state packed into
+// 64 bits: epoch (16) | rows that have sighted it (16) | ~T (32).  Rows
+// 1..n-1 then pass over [0, M) in order; row k's sighting at s of a word rows
+// 0..k-1 all have sighted raises it to k+1 rows with T = max(T, s) by
+// atomicMax -- the packing makes the higher row count win and, among equal
+// counts, the smaller T: the row's FIRST sighting.  A step takes 512 shifts
+// (8 per lane) in increasing order and reads every state before any of its
+// atomics, so a word raised by an earlier step of the pass is never raised
+// again.  A row pass that raises nothing ends the prefix (S* >= M); the
+// last row's smallest T is S*.
+static constexpr int LW_STEP = 512;
+typedef __attribute__((address_space(3))) unsigned char LdsU8;
+
+struct LongOut {
+    int found, my_shift, shifts;  // found: 1, 0 (no shift works), -1 (the table cannot take a prefix)
+    uint32_t epoch;
+};
+
+// codes of chars q0 .. q0 + 575 of a row into LDS (7 past the row's end)
+__device__ __forceinline__ void lw_codes(const char* p, int len, int d, int q0, int lane, LdsU8* buf) {
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+        const int q = q0 + j * 64 + lane;
+        buf[j * 64 + lane] = q < len ? (unsigned char)Proc_code3((unsigned char)p[(ptrdiff_t)d * q]) : 7;
+    }
+}
+
+// words at shifts base + 8*lane + u, u < 8, from the codes of chars base + ...
+__device__ __forceinline__ void lw_words(const LdsU8* buf, int lane, int ac, unsigned long long wmask,
+                                         unsigned long long (&wd)[8]) {
+    const int sb = 8 * lane;
+    unsigned long long x = 0;
+    for (int t = 0; t < ac - 1; t++) x = (x << 3) | buf[sb + t];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        x = ((x << 3) | buf[sb + ac - 1 + u]) & wmask;
+        wd[u] = x;
+    }
+}
+
+__device__ __noinline__ LongOut find_word_long(const char* vp, int vlen, int vd, int pos, int lane, int n, int ac,
+                                               int max_shift, int M0, unsigned long long* W,
+                                               unsigned long long* tkeys, unsigned long long* tmask,
+                                               uint32_t tcap_log2, uint32_t epoch) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    ac = __builtin_amdgcn_readfirstlane(ac);
+    max_shift = __builtin_amdgcn_readfirstlane(max_shift);
+    M0 = __builtin_amdgcn_readfirstlane(M0);
+    tcap_log2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)tcap_log2);
+    epoch = (uint32_t)__builtin_amdgcn_readfirstlane((int)epoch);
+    LdsU8* buf = (LdsU8*)W;
+    LongOut out{0, 0, max_shift, epoch};
+    const bool act = lane < n;
+    const View v{vp, vlen, vd};
+    const unsigned long long wmask = (ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * ac)) - 1);
+    const unsigned long long EPM = ~((1ull << 48) - 1);
+    const uint32_t tcap = 1u << tcap_log2;
+    const uint32_t INV = 0xFFFFFFFFu;
+    int S = -1;
+    unsigned long long ep = 0;
+    for (int M = max(M0, LW_STEP);; M *= 2) {
+        const int Mp = min(M, max_shift);
+        if (2u * (uint32_t)Mp > tcap) {
+            out.found = -1;
+            return out;
+        }
+        uint32_t ep32 = out.epoch + 1;
+        if (ep32 >= 0xFFFF) {  // epoch wrap: clear the table
+            for (uint32_t i = lane; i < tcap; i += 64) {
+                tkeys[i] = 0ull;
+                tmask[i] = 0ull;
+            }
+            __threadfence();
+            ep32 = 1;
+        }
+        out.epoch = ep32;
+        ep = (unsigned long long)ep32 << 48;
+        bool alive = true;
+        int tmin = 0x7fffffff;
+        for (int k = 0; k < n && alive; k++) {
+            const char* pk = bcast_ptr(vp, k);
+            const int lk = bcast(vlen, k), dk = bcast(vd, k), qk = bcast(pos, k);
+            int any = 0;
+            for (int base = 0; base < Mp; base += LW_STEP) {
+                if (k == n - 1 && base > tmin) break;  // later shifts cannot lower the last row's T
+                __syncthreads();
+                lw_codes(pk, lk, dk, qk + base, lane, buf);
+                __syncthreads();
+                unsigned long long wd[8];
+                lw_words(buf, lane, ac, wmask, wd);
+                uint32_t slot[8];
+                bool valid[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    valid[u] = base + 8 * lane + u < Mp;
+                    slot[u] = (uint32_t)(((ep | wd[u]) * 0x9E3779B97F4A7C15ull) >> (64 - tcap_log2));
+                }
+                if (k == 0) {  // row 0: insert (claim the key, reset a new key's state)
+                    bool claimed[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        claimed[u] = false;
+                        if (!valid[u]) continue;
+                        const unsigned long long key = ep | wd[u];
+                        while (true) {
+                            unsigned long long kk =
+                                __hip_atomic_load(&tkeys[slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (kk == key) break;
+                            if ((kk & EPM) != ep) {
+                                if (__hip_atomic_compare_exchange_strong(&tkeys[slot[u]], &kk, key, __ATOMIC_RELAXED,
+                                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                                    claimed[u] = true;
+                                    break;
+                                }
+                                if (kk == key) break;
+                                continue;
+                            }
+                            slot[u] = (slot[u] + 1) & (tcap - 1);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; u++)
+                        if (claimed[u]) __hip_atomic_store(&tmask[slot[u]], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __threadfence();
+#pragma unroll
+                    for (int u = 0; u < 8; u++)
+                        if (valid[u])
+                            __hip_atomic_fetch_max(&tmask[slot[u]],
+                                                   ep | (1ull << 32) | (unsigned long long)(INV - (uint32_t)(base + 8 * lane + u)),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    any = 1;
+                } else {  // rows 1..n-1: raise the words rows 0..k-1 all have
+                    unsigned long long kk[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++)
+                        kk[u] = valid[u] ? __hip_atomic_load(&tkeys[slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : 0ull;
+                    bool hit[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const unsigned long long key = ep | wd[u];
+                        while (valid[u] && kk[u] != key && (kk[u] & EPM) == ep) {
+                            slot[u] = (slot[u] + 1) & (tcap - 1);
+                            kk[u] = __hip_atomic_load(&tkeys[slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        hit[u] = valid[u] && kk[u] == key;
+                    }
+                    unsigned long long st[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++)
+                        st[u] = hit[u] ? __hip_atomic_load(&tmask[slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0ull;
+                    const unsigned long long want = ep | ((unsigned long long)k << 32);
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        if (!hit[u] || (st[u] & ~0xFFFFFFFFull) != want) continue;
+                        const int s = base + 8 * lane + u;
+                        const int T = (int)(INV - (uint32_t)st[u]);
+                        const int t = max(T, s);
+                        __hip_atomic_fetch_max(&tmask[slot[u]],
+                                               ep | ((unsigned long long)(k + 1) << 32) | (unsigned long long)(INV - (uint32_t)t),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        any = 1;
+                        if (k == n - 1) tmin = min(tmin, t);
+                    }
+                    if (k == n - 1) tmin = wave_min(tmin);
+                }
+            }
+            __threadfence();  // this row's raises before the next row's reads
+            alive = ballot(any != 0) != 0ull;
+        }
+        if (alive) {
+            S = tmin;
+            break;
+        }
+        if (Mp >= max_shift) {
+            __syncthreads();
+            return out;  // no shift works
+        }
+    }
+    // the word: the highest row whose word at S* is complete
+    unsigned long long wi = 0;
+    if (act)
+        for (int t = 0; t < ac; t++) wi = (wi << 3) | Proc_code3(vch(v, pos + S + t, lane));
+    bool complete = false;
+    if (act) {
+        const unsigned long long key = ep | wi;
+        uint32_t sl = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tcap_log2));
+        while (true) {
+            const unsigned long long kk = __hip_atomic_load(&tkeys[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kk == key) {
+                const unsigned long long st = __hip_atomic_load(&tmask[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                complete = (st & ~0xFFFFFFFFull) == (ep | ((unsigned long long)n << 32)) &&
+                           (int)(INV - (uint32_t)st) <= S;
+                break;
+            }
+            if ((kk & EPM) != ep) break;
+            sl = (sl + 1) & (tcap - 1);
+        }
+    }
+    const unsigned long long cm = ballot(complete);
+    const int ib = cm ? 63 - __clzll((long long)cm) : 0;
+    const unsigned long long best = bcast64(wi, ib);
+    int my_shift = S;
+    if ((ballot(act && wi != best)) != 0ull) {
+        // first sightings of the word: each row's shifts [0, S] in steps
+        for (int k = 0; k < n; k++) {
+            const char* pk = bcast_ptr(vp, k);
+            const int lk = bcast(vlen, k), dk = bcast(vd, k), qk = bcast(pos, k);
+            int f = 0x7fffffff;
+            for (int base = 0; base <= S && f == 0x7fffffff; base += LW_STEP) {
+                __syncthreads();
+                lw_codes(pk, lk, dk, qk + base, lane, buf);
+                __syncthreads();
+                unsigned long long wd[8];
+                lw_words(buf, lane, ac, wmask, wd);
+                int g = 0x7fffffff;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int s = base + 8 * lane + u;
+                    if (s <= S && wd[u] == best) g = min(g, s);
+                }
+                f = wave_min(g);
+            }
+            if (lane == k) my_shift = f;
+        }
+    }
+    __syncthreads();
+    out.found = 1;
+    out.my_shift = my_shift;
+    out.shifts = S + 1;
+    return out;
+}
+
 
 // ---------------------------------------------------------------- process_seqs
 struct Proc {
@@ -752,8 +1004,12 @@ struct Proc {
         const int max_shift = mt - P.ac;
         if (max_shift <= 0) return false;
         n_aligned_calls++;
+        // the first P.lh shifts incrementally (most searches end there), then
+        // whole prefixes (find_word_long)
+        const bool lng = P.lh > 0 && w.n >= 2 && max_shift > P.lh;
+        const int head = lng ? P.lh : max_shift;
         if (w.n <= VEC_ROWS) {
-            const VecOut r = find_word_vec(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, max_shift, S.lwords, S.tkeys,
+            const VecOut r = find_word_vec(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, head, S.lwords, S.tkeys,
                                            S.tmask, S.tcap_log2, epoch);
             epoch = r.epoch;
             n_shifts += r.shifts;
@@ -765,11 +1021,25 @@ struct Proc {
 #endif
             if (r.found > 0) my_shift = r.my_shift;
             if (r.found < 0) table_full();
-            return r.found > 0;
+            if (r.found != 0 || !lng) return r.found > 0;
+        } else {
+            const int r = find_word<LdsU64, LdsU32>(my_shift, head, (LdsU64*)S.lkeys, (LdsU64*)S.lmask,
+                                                    (LdsU32*)S.ldone, S.ltab_log2, lepoch, 1 << (S.ltab_log2 - 1));
+            if (r == 1 || (r == 0 && !lng)) return r == 1;
+            if (r < 0) {
+                const int g = find_word<unsigned long long, uint32_t>(my_shift, head, S.tkeys, S.tmask, S.tdone,
+                                                                      S.tcap_log2, epoch, (1 << (S.tcap_log2 - 1)) - 64);
+                if (g < 0) table_full();
+                if (g != 0 || !lng) return g == 1;
+            }
         }
-        const int r = find_word<LdsU64, LdsU32>(my_shift, max_shift, (LdsU64*)S.lkeys, (LdsU64*)S.lmask,
-                                                (LdsU32*)S.ldone, S.ltab_log2, lepoch, 1 << (S.ltab_log2 - 1));
-        if (r >= 0) return r == 1;
+        const LongOut L = find_word_long(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, max_shift, P.lm, S.lwords,
+                                         S.tkeys, S.tmask, S.tcap_log2, epoch);
+        epoch = L.epoch;
+        n_shifts += L.shifts - head;
+        if (L.found > 0) my_shift = L.my_shift;
+        if (L.found >= 0) return L.found > 0;
+        // a prefix the table cannot take: every shift incrementally
         const int g = find_word<unsigned long long, uint32_t>(my_shift, max_shift, S.tkeys, S.tmask, S.tdone,
                                                               S.tcap_log2, epoch, (1 << (S.tcap_log2 - 1)) - 64);
         if (g < 0) table_full();

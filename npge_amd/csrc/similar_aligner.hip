@@ -2422,6 +2422,12 @@ struct npgx_aligner {
     // least two rows are cut every `split` columns of their longest row
     // (NPGX_ALIGN_SPLIT; 0: never)
     int split = 384;
+    // try_aligned's word search: the first `long_head` shifts incrementally,
+    // then whole prefixes from `long_m` shifts on (find_word_long,
+    // sa_device.hpp; NPGX_LONG_HEAD / NPGX_LONG_M; long_head 0: incremental
+    // only, the round-4 search)
+    int long_head = 32;
+    int long_m = 512;
     // twins of the split jobs (NPGX_TWINS: 0 never -- the default: measured at
     // C3 and C5 the whole-job bad region they serve is rare among split jobs
     // and their segments slow the launch -- 1 always, -1 in launches with few
@@ -2640,7 +2646,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     };
     put(al->d_row_off.p, ne_off.data(), ne_off.size() * 8);
     put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
-    Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf};
+    Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf, al->long_head, al->long_m};
 
     std::vector<int32_t>& jlen = al->h_jlen;
     std::vector<int32_t>& jstat = al->h_jstat;
@@ -3267,13 +3273,15 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         pmark(8);
         int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);
         NPGX_HIP(hipMemcpyAsync(pl, d_job_len, ((size_t)n_jobs * 2 + 1) * 4, hipMemcpyDeviceToHost, st));
-        if (al->want_stats)
-            NPGX_HIP(hipMemcpyAsync(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost, st));
         al->host_ms[0] += ms(tp);
         tp = std::chrono::steady_clock::now();
         NPGX_HIP(stream_wait(st));
         al->host_ms[1] += ms(tp);
         tp = std::chrono::steady_clock::now();
+        // (after the wait: a copy into pageable memory would wait for the
+        // kernels itself and book their time as host preparation)
+        if (al->want_stats)
+            NPGX_HIP(hipMemcpy(jst.data(), al->d_job_stats.p, jst.size() * 8, hipMemcpyDeviceToHost));
         memcpy(jlen.data(), pl, n_jobs * 4);
         memcpy(jstat.data(), pl + n_jobs, n_jobs * 4);
         al->epoch_base = std::max(al->epoch_base, (uint32_t)pl[2 * n_jobs] + 1);
@@ -3439,6 +3447,10 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         if (dr && *dr) a->defer_rows = std::max(0, atoi(dr));
         const char* sp = getenv("NPGX_ALIGN_SPLIT");
         if (sp && *sp) a->split = std::max(0, atoi(sp));
+        const char* lh = getenv("NPGX_LONG_HEAD");
+        if (lh && *lh) a->long_head = std::max(0, atoi(lh));
+        const char* lm = getenv("NPGX_LONG_M");
+        if (lm && *lm) a->long_m = std::max(64, atoi(lm));
         const char* tw = getenv("NPGX_TWINS");
         if (tw && *tw) a->twins = atoi(tw) > 0 ? 1 : (atoi(tw) == 0 ? 0 : -1);
         const char* sb = getenv("NPGX_SLOT_BUDGET_MB");

@@ -1,0 +1,114 @@
+"""The device ExtendLoopFast (npge_amd/csrc/elf_device.inc):
+block table, block_hash, MoveUnchanged, flank plan, stitch, FixEnds slicing,
+OverlaplessUnion and the Pipe state on the GPU.
+
+* OverlaplessUnion@device (the loop's OverlaplessUnion on arbitrary blocks)
+  against the oracle's OverlaplessUnion (OverlaplessUnion.cpp:25-80): sparse,
+  dense and long-fragment sets, many sequences, equal sizes and lengths
+  (the pinned tie-breaks decide), and the inputs the device hands to the
+  host (blocks overlapping themselves: SetFc's multiset mode).
+* ExtendLoopFast / DraftPangenome with the device loop against the host loop
+  (NPGX_ELF_DEVICE=0) and the oracle: fragments, rows, stats.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from npge_amd import synth
+
+from test_block_build_gpu import _engine, _ou_blocks, _stem_blocks, canon
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("max_len,self_overlap", [(40, False), (400, False), (3000, False), (40, True),
+                                                  (400, 60)])
+def test_ou_device_many_blocks(max_len, self_overlap):
+    rng = np.random.default_rng(max_len + 7 * int(self_overlap))
+    n_seqs, seq_len = 8, 400000
+    seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
+    names = ["g%d&c&c" % i for i in range(n_seqs)]
+    blocks = _ou_blocks(rng, n_seqs, seq_len, 1500, max_len, self_overlap)
+    ss, eng = _engine(seqs, names)
+    o = orc.BlockSetOracle(seqs, names)
+    eng.set_blocks(blocks).apply("OverlaplessUnion@device")
+    o.set_blocks(blocks)
+    o.apply("OverlaplessUnion")
+    want = o.blocks()
+    assert eng.blocks() == want
+    assert 0 < len(want) <= len(blocks)
+
+
+def test_ou_device_ties_and_chains():
+    """Blocks of equal size and length (the minimum fragment, then the sorted
+    fragment list, then the input order decide) in long overlap chains (the
+    priority sweeps run many rounds), and blocks without fragments in range
+    of nothing else."""
+    rng = np.random.default_rng(5)
+    n_seqs, seq_len = 3, 200000
+    seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
+    names = ["t%d&c&c" % i for i in range(n_seqs)]
+    blocks = []
+    for i in range(2000):  # a chain along sequence 0: each block overlaps the next
+        a = 50 * i
+        blocks.append([(0, a, a + 60, 1, None), (1 + i % 2, a, a + 60, -1 if i % 3 else 1, None)])
+    for i in range(300):  # duplicates of earlier blocks' first fragments
+        j = int(rng.integers(0, 2000))
+        blocks.append([blocks[j][0], (2, 150000 + 70 * i, 150000 + 70 * i + 60, 1, None)])
+    perm = rng.permutation(len(blocks))
+    blocks = [blocks[int(k)] for k in perm]
+    ss, eng = _engine(seqs, names)
+    o = orc.BlockSetOracle(seqs, names)
+    eng.set_blocks(blocks).apply("OverlaplessUnion@device")
+    o.set_blocks(blocks)
+    o.apply("OverlaplessUnion")
+    assert eng.blocks() == o.blocks()
+
+
+def test_ou_device_many_sequences():
+    rng = np.random.default_rng(12)
+    n_seqs, seq_len = 4000, 1200
+    seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
+    names = ["c%d&c&c" % i for i in range(n_seqs)]
+    blocks = _ou_blocks(rng, n_seqs, seq_len, 2500, 600, False)
+    ss, eng = _engine(seqs, names)
+    o = orc.BlockSetOracle(seqs, names)
+    eng.set_blocks(blocks).apply("OverlaplessUnion@device")
+    o.set_blocks(blocks)
+    o.apply("OverlaplessUnion")
+    assert eng.blocks() == o.blocks()
+
+
+def _draft(cfg, device, monkeypatch):
+    from npge_amd.anchor_finder import AnchorFinder
+    monkeypatch.setenv("NPGX_ELF_DEVICE", "1" if device else "0")
+    names, seqs = synth.genome_set(cfg)
+    ss, eng = _engine(seqs, names)
+    eng.apply("DraftPangenome", af=AnchorFinder())
+    st = eng.stats()
+    return eng.blocks(), eng.rows_digest(), st
+
+
+@pytest.mark.parametrize("cfg", ["tiny", "small", "rtiny", "rsmall"])
+def test_draft_device_equals_host_loop(cfg, monkeypatch):
+    b_dev, d_dev, s_dev = _draft(cfg, True, monkeypatch)
+    b_host, d_host, s_host = _draft(cfg, False, monkeypatch)
+    assert canon(b_dev) == canon(b_host)
+    assert d_dev == d_host
+    for k in ("iterations", "aligned_residues", "align_jobs", "stem_blocks"):
+        assert s_dev[k] == s_host[k], k
+
+
+@pytest.mark.parametrize("cfg,iters", [("tiny", 10), ("small", 2), ("rtiny", 10)])
+def test_extend_loop_fast_device_vs_oracle(cfg, iters, monkeypatch):
+    monkeypatch.setenv("NPGX_ELF_DEVICE", "1")
+    names, seqs = synth.genome_set(cfg)
+    b0 = _stem_blocks(seqs, names)
+    ss, eng = _engine(seqs, names, max_iterations=iters)
+    o = orc.BlockSetOracle(seqs, names, max_iterations=iters)
+    eng.set_blocks(b0).apply("ExtendLoopFast")
+    o.set_blocks(b0)
+    o.apply("ExtendLoopFast")
+    assert eng.stats()["iterations"] == o.stats()["iterations"]
+    assert canon(eng.blocks()) == canon(o.blocks())
+    assert eng.hash() == o.hash()

@@ -326,3 +326,54 @@ def test_wide_unrelated_long_tails():
         tail = rng.integers(0, 4, int(rng.integers(20000, 21000)))
         rows.append("".join("ATGC"[x] for x in np.concatenate([c, tail])))
     _check([rows])
+
+
+def _restart_family(rng, n, core, ins, d=0.01, repeat=0.0):
+    """Rows that agree, then each carry an unrelated insertion of up to `ins`
+    bases at the same place, then agree again: try_aligned searches past the
+    insertions (hundreds to thousands of shifts).  With `repeat`, the
+    insertions also hold copies of the next words of the shared text, so the
+    search meets complete words at several shifts (first sightings, the
+    highest-row rule and words.size() == 1 all decide)."""
+    anc = "".join("ATGC"[x] for x in rng.integers(0, 4, 2 * core + 40))
+    rows = []
+    for _ in range(n):
+        left = list(anc[:core])
+        right = list(anc[core:])
+        for part in (left, right):
+            for i in range(len(part)):
+                if rng.random() < d:
+                    part[i] = "ATGC"[int(rng.integers(0, 4))]
+        k = int(rng.integers(0, ins + 1))
+        mid = "".join("ATGC"[x] for x in rng.integers(0, 4, k))
+        if repeat and k > 40 and rng.random() < repeat:
+            a = int(rng.integers(0, k - 20))
+            mid = mid[:a] + anc[core:core + 20] + mid[a + 20:]
+        rows.append("".join(left) + mid + "".join(right))
+    return rows
+
+
+@pytest.mark.parametrize("head,m", [("32", "512"), ("0", "512"), ("1", "64"), ("64", "2048")])
+def test_long_restart_searches(head, m, monkeypatch):
+    """try_aligned's prefix search (find_word_long, sa_device.hpp) against the
+    oracle's find_best_word loop: unrelated insertions of up to 6000 bases
+    between shared stretches, 2 to 40 rows (the vector search up to 8 rows,
+    the row-parallel one above), repeats planted in the insertions, low-
+    complexity inserts (many equal words), and no shared word at all.
+    NPGX_LONG_HEAD / NPGX_LONG_M move the switch from the incremental search
+    (0: never switch) and the first prefix."""
+    monkeypatch.setenv("NPGX_LONG_HEAD", head)
+    monkeypatch.setenv("NPGX_LONG_M", m)
+    rng = np.random.default_rng(51)
+    jobs = []
+    for n in (2, 3, 5, 8, 9, 17, 40):
+        for ins, rep in ((300, 0.0), (2000, 0.5), (6000, 0.0), (1500, 1.0)):
+            jobs.append(_restart_family(rng, n, 300, ins, repeat=rep))
+    for n in (2, 12):  # low-complexity insertions: poly-A and a dinucleotide repeat
+        core = "".join("ATGC"[x] for x in rng.integers(0, 4, 400))
+        jobs.append([core[:200] + "A" * int(rng.integers(100, 900)) + core[200:] for _ in range(n)])
+        jobs.append([core[:200] + "AT" * int(rng.integers(50, 700)) + core[200:] for _ in range(n)])
+    for n in (2, 10):  # nothing shared after the core: the search runs out
+        core = "".join("ATGC"[x] for x in rng.integers(0, 4, 150))
+        jobs.append([core + "".join("ATGC"[x] for x in rng.integers(0, 4, 3000)) for _ in range(n)])
+    _check(jobs)

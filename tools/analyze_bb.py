@@ -58,7 +58,6 @@ js = eng.job_stats()
 os.makedirs("gpurun_out", exist_ok=True)
 np.save("gpurun_out/jobstats_%s%s.npy" % (cfg, "_prof" if os.environ.get("NPGX_PROFILE") == "1" else ""), js)
 cyc, cols, calls, shifts, gaps, regions, rows, fast = js.T[:8]
-ph = js[:, 8:]
 print("jobs", len(js), "total cycles %.3e" % cyc.sum(), "columns", cols.sum(), "shifts", shifts.sum(),
       "aligned calls", calls.sum(), "gaps", gaps.sum())
 order = np.argsort(-cyc)
@@ -66,12 +65,19 @@ print("top jobs by cycles (cycles, cols, calls, shifts, gaps, regions, rows, fas
 for i in order[:25]:
     print("  ", cyc[i], cols[i], calls[i], shifts[i], gaps[i], regions[i], rows[i], fast[i],
           round(cyc[i] / max(cols[i], 1), 1))
-names = ["process_seqs", "fix_bad_regions", "realing_end", "remove_gaps", "fast_run", "eq/mismatch",
-         "try_gap", "try_aligned"]
+# job-stat columns (include/npge_amd.h npgx_align_job_stats): 8-10 the phases
+# process_seqs / fix_bad_regions / realing_end, 11 and 23 wall-clock start and
+# end (not cycles), 12-21 the profiling build's Proc counters, 22 regions
+names = ["process_seqs", "fix_bad_regions", "realing_end"]
+prof_names = ["fast_run", "eq/mismatch", "try_gap", "try_aligned", "vec_words", "vec_compares",
+              "vec_chunks", "vec_calls", "append_end", "child_return"]
+cols_ph = [8, 9, 10] + list(range(12, 22)) + [22]
+all_names = names + prof_names + ["regions"]
+ph = js[:, cols_ph]
 tot = ph.sum(axis=0)
-print("phase cycles (all jobs):", {n: "%.3e" % t for n, t in zip(names, tot)})
+print("phase cycles (all jobs):", {n: "%.3e" % t for n, t in zip(all_names, tot)})
 for i in order[:5]:
-    print("  top job phases:", {n: int(t) for n, t in zip(names, ph[i])})
+    print("  top job phases:", {n: int(t) for n, t in zip(all_names, ph[i])})
 print("cycles per column (median, p90, p99):", np.percentile(cyc / np.maximum(cols, 1), [50, 90, 99]))
 if shifts.sum():
     m = shifts > 0

@@ -207,6 +207,9 @@ def main():
         ach = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "kernel": dom["name"],
+                    "kernel_scope": "the longest of the HIP-event-timed launches (NPGX_TIMERS=1: the aligner's "
+                                    "k_align_jobs / k_align_wide); every kernel of the step is ranked in the "
+                                    "rocprofv3 kernel-stats summaries under profiles/",
                     "launches_per_step": dom["launches"],
                     "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                     "bytes_per_launch": dom["bytes"] / dom["launches"]}

@@ -59,7 +59,9 @@ typedef struct {
  * with an N bitmap.  Input strings go through Sequence::to_atgcn
  * (uppercase, IUPAC -> N, other characters dropped).  Sequences are ranked by
  * (size desc, name asc, input index asc) -- the pinned form of the reference's
- * unstable size sort (SeqI.hpp:54).  names may be NULL (empty names). */
+ * unstable size sort (SeqI.hpp:54).  names may be NULL (empty names).
+ * Thread-safe; creations of sets up to 256 MiB of text share one pinned
+ * staging buffer and run their upload one at a time. */
 int npgx_seqset_create(const char* const* seqs, const int64_t* lens,
                        const char* const* names, int32_t n, npgx_seqset** out);
 int npgx_seqset_count(const npgx_seqset* s, int32_t* n);
@@ -332,7 +334,9 @@ typedef struct {
     double ms_stage[16];
     /* 0 blocks after ExtendLoopFast, 1 blocks passing Filter whole, 2 blocks
      * sent to goodSlices, 3 blocks after Filter, 4 blocks into OverlaplessUnion
-     * (all iterations), 5 of them rejected, 6 block hashes computed */
+     * (all iterations), 5 of them rejected, 6 block hashes computed (host), 7
+     * ExtendLoopFast on the device: OverlaplessUnion runs handed to the host
+     * (AnchorLoop: AddingLoopBySize rounds) */
     int64_t counters[8];
     /* AnchorLoopFast: 0 consensus sequences, 1 anchor blocks on them, 2
      * consensus blocks after the pipe's ExtendLoopFast, 3 blocks DeConSeq

@@ -330,13 +330,23 @@ int npgx_seqset_create(const char* const* seqs, const int64_t* lens, const char*
         for (int32_t i = 0; i < n; i++) ascii[i + 1] = ascii[i] + (int64_t)s->data[i].size();
         DevBuf<unsigned char> d_ascii;
         d_ascii.ensure((size_t)std::max<int64_t>(ascii[n], 1));
-        if (ascii[n] > 0) {
+        // sets up to 256 MiB share one pinned staging buffer (kept, so repeated
+        // creations skip the pinning; creations of such sets serialize on it);
+        // larger ones pin a buffer of their own for the call, so the largest
+        // set ever uploaded does not stay pinned in host memory
+        static constexpr int64_t SHARED_STAGING_MAX = 256ll << 20;
+        auto stage_copy = [&](char* st) {
+            heavy_for((size_t)n, ascii[n], [&](size_t i) { memcpy(st + ascii[i], s->data[i].data(), s->data[i].size()); });
+            NPGX_HIP(hipMemcpy(d_ascii.p, st, (size_t)ascii[n], hipMemcpyHostToDevice));
+        };
+        if (ascii[n] > SHARED_STAGING_MAX) {
+            PinnedBuf<char> own;
+            stage_copy(own.ensure((size_t)ascii[n]));
+        } else if (ascii[n] > 0) {
             static std::mutex mu;
             static PinnedBuf<char> staging;
             std::lock_guard<std::mutex> lk(mu);
-            char* st = staging.ensure((size_t)ascii[n]);
-            heavy_for((size_t)n, ascii[n], [&](size_t i) { memcpy(st + ascii[i], s->data[i].data(), s->data[i].size()); });
-            NPGX_HIP(hipMemcpy(d_ascii.p, st, (size_t)ascii[n], hipMemcpyHostToDevice));
+            stage_copy(staging.ensure((size_t)ascii[n]));
         }
         pack_device(s.get(), d_ascii.p, ascii);
         s->ms_upload = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();

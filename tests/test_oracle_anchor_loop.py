@@ -80,3 +80,32 @@ def test_anchor_loop_deterministic_and_aligned():
     assert res[0] == res[1]
     st = res[0][1]
     assert st["cons_seqs"] > 0 and st["cons_anchors"] > 0 and st["split_blocks"] > 0
+
+
+def test_anchor_loop_invariants_whatever_the_pinned_choices():
+    """Properties of the AnchorLoop result that hold whatever the conventions
+    this port pins where the reference is not reproducible (the consensus
+    sequences' fresh names, SplitExtendable's std::set<Fragment*> order, the
+    sort tie-breaks; DESIGN.md "The AnchorLoop pipe"): every block's rows
+    have one length and hold its fragments' letters, the closing Align's
+    Filter leaves every block as it is, and every DraftPangenome block the
+    pipe started from is still there (on rtiny; the result may overlap
+    itself: the consensus blocks DeConSeq maps back are not unioned against
+    them)."""
+    names, seqs = synth.genome_set("rtiny")
+    o = orc.BlockSetOracle(seqs, names)
+    o.apply("DraftPangenome")
+    draft = {tuple(sorted(f[:4] for f in b)) for b in o.blocks()}
+    o.apply("AnchorLoop")
+    out = o.blocks()
+    assert out
+    for b in out:
+        rows = [f[4] for f in b]
+        assert all(r is not None and len(r) == len(rows[0]) for r in rows)
+        for (q, mn, mx, ori, row) in b:
+            assert len(row) - row.count("-") == mx - mn + 1
+    f2 = orc.BlockSetOracle(seqs, names)
+    f2.set_blocks(out)
+    f2.apply("Filter")
+    assert sorted(tuple(sorted(b)) for b in f2.blocks()) == sorted(tuple(sorted(b)) for b in out)
+    assert draft <= {tuple(sorted(f[:4] for f in b)) for b in out}

@@ -28,7 +28,8 @@ def _stale(lib=LIB):
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False, profile=False, lib_path=None):
+def build(force=False, verbose=False, profile=False, lib_path=None, defines=()):
+    """defines: extra -D flags for an A/B variant (e.g. ("SA_FAST_ROWS=1",))."""
     lib = lib_path or (LIB_PROF if profile else LIB)
     if not force and not _stale(lib):
         return lib
@@ -42,7 +43,8 @@ def build(force=False, verbose=False, profile=False, lib_path=None):
         else:
             cmd = ["hipcc", "-c", "-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
                    "-munsafe-fp-atomics", "-Wno-unused-result", "-I", os.path.join(os.path.dirname(HERE), "include"),
-                   "-o", obj, os.path.join(CSRC, src)] + (["-DNPGX_SA_PROFILE=1"] if profile else [])
+                   "-o", obj, os.path.join(CSRC, src)] + (["-DNPGX_SA_PROFILE=1"] if profile else []) + \
+                  ["-D" + d for d in defines]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -278,8 +278,23 @@ struct AlignResult {
     std::vector<const char*> bptr;     // device address of the job's first output row
     std::vector<int64_t> row_ne;       // batch row -> index among its job's non-empty rows (-1: empty)
 };
+// job j's gapped rows on the device: row k at p + k * stride, len columns
+struct JobRows {
+    const char* p;
+    int32_t stride, len;
+};
+// align_device without a host wait (the device ExtendLoopFast): the jobs that
+// overflow the first attempt re-run at the proven bound in the same stream
+// (their list made on the device), and every job's result goes to `out`
+// (device, one JobRows per job); `err` (device) is set when a job overflows
+// both attempts.  No job may have more than 64 non-empty rows (k_align_wide
+// is host-driven); AlignResult is left empty.
+struct AlignAsync {
+    JobRows* out;
+    int32_t* err;
+};
 void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, const int32_t* row_len,
-                  const int32_t* job_row_start, int32_t n_jobs, AlignResult& res);
+                  const int32_t* job_row_start, int32_t n_jobs, AlignResult& res, const AlignAsync* as = nullptr);
 // wide_aligner.hip: align_seqs for problems of more than 64 non-empty rows (one
 // workgroup per problem); results stay in the WideBufs (row r at ptr + r * cap)
 struct WideJobIn {

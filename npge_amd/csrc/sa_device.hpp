@@ -71,6 +71,10 @@ struct Slot {
 };
 
 static constexpr int VEC_ROWS = 8;
+#ifndef SA_FAST_ROWS
+#define SA_FAST_ROWS 4
+#endif
+static constexpr int FR = SA_FAST_ROWS;  // fast_run: rows loaded per batch
 typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // LDS-qualified word-table entry
 typedef __attribute__((address_space(3))) uint32_t LdsU32;
 static constexpr int HIST_SHIFTS = 32;  // words per lane kept for the first-sighting scan  // try_aligned with lanes = shifts up to this many rows
@@ -864,14 +868,32 @@ struct Proc {
                 const char c0 = valid ? p0[(ptrdiff_t)d0 * (q0 + j)] : 0;
                 ob[col + j] = c0;  // speculative: columns past the consumed ones are rewritten later
                 bool eq = true;
-                for (int r = 1; r < w.n; r++) {
-                    const char* pr = bcast_ptr(v.p, r);
-                    const int dr = bcast(v.d, r), lr = bcast(v.len, r), qr = bcast(pos, r);
-                    const bool vr = qr + j < lr;
-                    const char c = vr ? pr[(ptrdiff_t)dr * (qr + j)] : 0;
-                    ob[(size_t)r * cap + col + j] = c;
-                    valid &= vr;
-                    eq &= c == c0;
+                // FR rows' loads in flight before their stores: a store the
+                // compiler cannot prove apart from the next row's load would
+                // otherwise hold every load back a full latency (the rows never
+                // alias the output: they are the job's input, a stage or C)
+                for (int r0 = 1; r0 < w.n; r0 += FR) {
+                    char cb[FR];
+#pragma unroll
+                    for (int u = 0; u < FR; u++) {
+                        const int r = r0 + u;
+                        cb[u] = 0;
+                        if (r < w.n) {
+                            const char* pr = bcast_ptr(v.p, r);
+                            const int dr = bcast(v.d, r), lr = bcast(v.len, r), qr = bcast(pos, r);
+                            const bool vr = qr + j < lr;
+                            cb[u] = vr ? pr[(ptrdiff_t)dr * (qr + j)] : 0;
+                            valid &= vr;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < FR; u++) {
+                        const int r = r0 + u;
+                        if (r < w.n) {
+                            ob[(size_t)r * cap + col + j] = cb[u];
+                            eq &= cb[u] == c0;
+                        }
+                    }
                 }
                 vm = ballot(valid);
                 em = ballot(valid && eq);

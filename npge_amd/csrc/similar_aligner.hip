@@ -90,6 +90,7 @@ struct SaArgs {
     const SaJob* jobs;
     const int32_t* order;      // job processing order (heaviest first)
     int32_t n_jobs;
+    const int32_t* n_jobs_dev; // non-null: the job count is on the device (the re-run of align_device's async mode)
     int32_t aligner_type;      // 0 similar, 1 dummy
     unsigned char* scratch;
     int32_t* job_len;
@@ -1985,13 +1986,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
     Slot& S = e.S;
     char* stage = e.stage;
     uint32_t lepoch = 0;
-    uint32_t epoch = a.epoch_base;
+    // above every epoch an earlier launch of this batch reached (slot_epoch is
+    // zeroed before a batch's first launch)
+    uint32_t epoch = next_epoch(a);
+    const unsigned int n_jobs = a.n_jobs_dev ? (unsigned)*a.n_jobs_dev : (unsigned)a.n_jobs;
 
     while (true) {
         unsigned int jn = 0;
         if (lane == 0) jn = atomicAdd(a.next_job, 1u);
         jn = bcast(jn, 0);
-        if (jn >= (unsigned)a.n_jobs) break;
+        if (jn >= n_jobs) break;
         const int oj = a.order[jn];
         // oj < 0: segment task -oj-1 of a split job -- process_seqs of the row
         // suffixes from its sync state into its own output; the wave that
@@ -2353,6 +2357,32 @@ __global__ void k_scatter(const unsigned char* __restrict__ blob, int n_ops) {
     }
 }
 
+// align_device's async mode: the jobs the first attempt overflowed (status
+// 1) listed for the re-run at the proven bound
+__global__ void k_retry_list(const int32_t* __restrict__ status, int32_t n, int32_t* __restrict__ order,
+                             int32_t* __restrict__ count, uint8_t* __restrict__ retried) {
+    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const bool r = status[j] == 1;
+    retried[j] = r;
+    if (r) order[atomicAdd(count, 1)] = j;
+}
+// ... and every job's rows (B of its A|B|C scratch, or A for status 2) from
+// the attempt that finished it
+__global__ void k_job_rows(const SaJob* __restrict__ jobs0, const SaJob* __restrict__ jobs1,
+                           const uint8_t* __restrict__ retried, const int32_t* __restrict__ status,
+                           const int32_t* __restrict__ len, int32_t n, const unsigned char* scratch0,
+                           const unsigned char* scratch1, JobRows* __restrict__ out, int32_t* __restrict__ err) {
+    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const bool r = retried[j];
+    const SaJob J = r ? jobs1[j] : jobs0[j];
+    const int32_t st = status[j];
+    if (st != 0 && st != 2) atomicOr(err, 1);
+    out[j] = JobRows{(const char*)((r ? scratch1 : scratch0) + J.scratch + (st == 2 ? 0 : (int64_t)J.n * J.cap)),
+                     J.cap, len[j]};
+}
+
 int weight_factor(int64_t min_identity_x1e4) {
     // FindLowSimilar::get_weight_factor with Decimal arithmetic (Decimal.hpp)
     int64_t mi = std::min<int64_t>(min_identity_x1e4, 9900);
@@ -2475,6 +2505,14 @@ struct npgx_aligner {
     std::vector<npgx::ScatterOp> h_ops;
     std::vector<unsigned char> h_blob;
     DevBuf<unsigned char> d_blob;
+    // async mode (AlignAsync): the re-run's jobs, list, counters, flags; the
+    // last launch's highest epoch copied back for the next call
+    std::vector<npgx::SaJob> h_jobs1;
+    DevBuf<SaJob> d_jobs1;
+    DevBuf<int32_t> d_order1, d_ctr1;
+    DevBuf<uint8_t> d_retried;
+    PinnedBuf<uint32_t> h_epoch;
+    bool epoch_pending = false;
 };
 
 namespace npgx {
@@ -2483,8 +2521,12 @@ namespace npgx {
 // (host arrays describing device memory).  Results stay on the device: job j's
 // non-empty row k is at res.bptr[j] + k*res.cap[j] for res.len[j] columns.
 void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, const int32_t* row_len,
-                  const int32_t* job_row_start, int32_t n_jobs, AlignResult& res) {
+                  const int32_t* job_row_start, int32_t n_jobs, AlignResult& res, const AlignAsync* as) {
     NPGX_HIP(hipSetDevice(al->device));
+    if (al->epoch_pending) {  // the last async call's highest epoch (its copy is complete: the caller synced)
+        al->epoch_base = std::max(al->epoch_base, al->h_epoch.p[0] + 1);
+        al->epoch_pending = false;
+    }
     auto tp = std::chrono::steady_clock::now();
     auto ms = [](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -2659,6 +2701,43 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     res.bptr.assign(n_jobs, nullptr);
     for (int32_t j = 0; j < n_jobs; j++) res.n[j] = jobs[j].n;
     std::vector<int32_t> todo = order;
+    // async mode: the re-run at the proven bound is planned now for every job
+    // (the device picks the ones that overflow), and the first attempt's
+    // buffers are sized to hold it too (nothing may be reallocated under the
+    // kernels in flight)
+    int64_t scratch1 = 0;
+    uint32_t tlog1 = 10;
+    int depth1 = 4, cols1 = 256;
+    size_t slots1 = 1;
+    if (as) {
+        NPGX_REQUIRE(wide_idx.empty(), NPGX_ERR_ARG, "align_device async: problems of more than 64 rows");
+        std::vector<SaJob>& j1 = al->h_jobs1;
+        j1 = jobs;
+        int mn = 1, ml = 1, mc = 1;
+        for (int32_t j : order) {
+            SaJob& J = j1[j];
+            int64_t sum = 0;
+            for (int i = 0; i < J.n; i++) sum += ne_len[J.row0 + i];
+            J.cap = (int32_t)((std::max<int64_t>(sum, 1) + 15) & ~15ll);
+            J.scratch = scratch1;
+            scratch1 += (3ll * J.n * J.cap + 255) & ~255ll;
+            mn = std::max(mn, J.n);
+            ml = std::max(ml, jmax[j]);
+            mc = std::max(mc, J.cap);
+        }
+        while ((1ull << tlog1) < 2ull * (uint64_t)mn * (uint64_t)(ml + 1) + 64) tlog1++;
+        depth1 = ml / std::max(1, o.aligned_check + 1) + 4;
+        cols1 = std::max(256, mc + 1);
+        const int64_t per1 = (20ll << tlog1) + 1028ll * depth1 + 17ll * cols1;
+        slots1 = (size_t)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>((int64_t)order.size(), 256),
+                                                                 std::max<int64_t>(al->slot_budget, 1ll << 22) / per1));
+        al->d_scratch2.ensure((size_t)std::max<int64_t>(scratch1, 256));
+        al->d_jobs1.ensure(jobs.size());
+        al->d_order1.ensure(std::max<size_t>(jobs.size(), 1));
+        al->d_ctr1.ensure(2);
+        al->d_retried.ensure(std::max<size_t>(jobs.size(), 1));
+        al->h_epoch.ensure(1);
+    }
     for (int attempt = 0; attempt < 2 && !todo.empty(); attempt++) {
         DevBuf<unsigned char>& scr = attempt == 0 ? al->d_scratch : al->d_scratch2;
         if (attempt == 1) {  // re-run overflowed jobs at the proven bound, in a second scratch
@@ -2835,23 +2914,26 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // at the last launch's highest epoch + 1), so entries left by earlier
         // launches never match, whatever the slot layout; the tables are
         // cleared only when they grow or the 16-bit epochs run out.
-        if (slots * tcap > al->tcap_alloc || al->epoch_base > 0xF000) {
-            al->tkeys.ensure(slots * tcap);
-            al->tmask.ensure(slots * tcap);
-            al->tdone.ensure(slots * tcap);  // reset when a key is claimed
+        const size_t tneed = as ? std::max(slots * tcap, slots1 * ((size_t)1 << tlog1)) : slots * tcap;
+        if (tneed > al->tcap_alloc || al->epoch_base > 0xF000) {
+            al->tkeys.ensure(tneed);
+            al->tmask.ensure(tneed);
+            al->tdone.ensure(tneed);  // reset when a key is claimed
             NPGX_HIP(hipMemsetAsync(al->tkeys.p, 0, al->tkeys.cap * 8, st));
             NPGX_HIP(hipMemsetAsync(al->tmask.p, 0, al->tmask.cap * 8, st));  // epoch-tagged masks (vector search)
-            al->tcap_alloc = std::max(al->tcap_alloc, slots * tcap);
+            al->tcap_alloc = std::max(al->tcap_alloc, tneed);
             al->epoch_base = 1;
         }
         zero(d_slot_epoch, 4);
-        al->st_p.ensure(slots * depth * 64);
-        al->st_len.ensure(slots * depth * 64);
-        al->st_pos.ensure(slots * depth * 64);
-        al->st_col.ensure(slots * depth);
+        const size_t sneed = as ? std::max(slots * depth, slots1 * depth1) : slots * depth;
+        al->st_p.ensure(sneed * 64);
+        al->st_len.ensure(sneed * 64);
+        al->st_pos.ensure(sneed * 64);
+        al->st_col.ensure(sneed);
         const int slot_cols = (int)cols_need;
-        al->regions.ensure(slots * (size_t)slot_cols);
-        al->good_col.ensure(slots * (size_t)slot_cols);
+        const size_t cneed = as ? std::max(slots * (size_t)slot_cols, slots1 * (size_t)cols1) : slots * (size_t)slot_cols;
+        al->regions.ensure(cneed);
+        al->good_col.ensure(cneed);
 
         pmark(4);
         SaArgs A;
@@ -2861,6 +2943,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.jobs = al->d_jobs.p;
         A.order = al->d_order.p;
         A.n_jobs = nj;
+        A.n_jobs_dev = nullptr;
         A.aligner_type = o.aligner_type;
         A.scratch = scr.p;
         A.job_len = d_job_len;
@@ -3073,6 +3156,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         pmark(6);
         int64_t residues = 0;
         for (int32_t j : todo) residues += jsum[j];
+        if (as) {
+            put(al->d_jobs1.p, al->h_jobs1.data(), al->h_jobs1.size() * sizeof(SaJob));
+            zero(al->d_ctr1.p, 8);
+        }
         flush();
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
                                     double(residues) * 2.0, residues);
@@ -3271,6 +3358,70 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             }
         }
         pmark(8);
+        if (as) {
+            // the overflowed jobs again at the proven bound (no splits, no
+            // deferred regions: attempt 1 of the synchronous path), then every
+            // job's rows
+            const unsigned jg = (unsigned)std::max<int64_t>(1, ((int64_t)n_jobs + 255) / 256);
+            hipLaunchKernelGGL(k_retry_list, dim3(jg), dim3(256), 0, st, d_job_status, n_jobs, al->d_order1.p,
+                               al->d_ctr1.p, al->d_retried.p);
+            SaArgs A1 = A;
+            A1.jobs = al->d_jobs1.p;
+            A1.order = al->d_order1.p;
+            A1.n_jobs = 0;
+            A1.n_jobs_dev = al->d_ctr1.p;
+            A1.next_job = (unsigned int*)(al->d_ctr1.p + 1);
+            A1.scratch = al->d_scratch2.p;
+            A1.tcap_log2 = tlog1;
+            A1.st_depth_max = depth1;
+            A1.slot_cols = cols1;
+            A1.defer = 0;
+            A1.job_regions = nullptr;
+            A1.job_nreg = nullptr;
+            A1.subs = nullptr;
+            A1.sub_res = nullptr;
+            A1.alloc = nullptr;
+            A1.counters = nullptr;
+            A1.pool = nullptr;
+            A1.pool_cap = 0;
+            A1.max_sub = 0;
+            A1.fin = nullptr;
+            A1.splits = nullptr;
+            A1.segs = nullptr;
+            A1.targets = nullptr;
+            A1.seg_res = nullptr;
+            A1.seg_wall = nullptr;
+            A1.sub_wall = nullptr;
+            A1.seg_pool = nullptr;
+            A1.sctr = nullptr;
+            A1.qseg = nullptr;
+            A1.qsub = nullptr;
+            A1.ftasks = nullptr;
+            A1.post_area = nullptr;
+            A1.chain = nullptr;
+            A1.chain_hdr = nullptr;
+            A1.chain_bits = nullptr;
+            A1.bits_off = nullptr;
+            A1.part0 = nullptr;
+            A1.split_len = 0;
+            A1.twin_rows = nullptr;
+            A1.twin_off = nullptr;
+            A1.cap_splits = A1.cap_segs = 0;
+            A1.cap_tgt = A1.cap_find = A1.cap_pool = 0;
+            size_t tr = al->timer.begin("align_jobs_retry", st, 0.0, 0);
+            hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
+            al->timer.end(tr, st);
+            hipLaunchKernelGGL(k_job_rows, dim3(jg), dim3(256), 0, st, al->d_jobs.p, al->d_jobs1.p, al->d_retried.p,
+                               d_job_status, d_job_len, n_jobs, scr.p, al->d_scratch2.p, as->out, as->err);
+            NPGX_HIP(hipGetLastError());
+            NPGX_HIP(hipMemcpyAsync(al->h_epoch.p, d_slot_epoch, 4, hipMemcpyDeviceToHost, st));
+            al->epoch_pending = true;
+            res.len.clear();
+            res.cap.clear();
+            res.bptr.clear();
+            al->host_ms[0] += ms(tp);
+            return;
+        }
         int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);
         NPGX_HIP(hipMemcpyAsync(pl, d_job_len, ((size_t)n_jobs * 2 + 1) * 4, hipMemcpyDeviceToHost, st));
         al->host_ms[0] += ms(tp);

@@ -322,7 +322,13 @@ void pack_device(npgx_seqset* s, const unsigned char* d_ascii, const std::vector
 }  // namespace npgx
 
 // ----------------------------------------------------------------- sequence set
+inline uint64_t npgx_next_uid() {
+    static std::atomic<uint64_t> n{0};
+    return ++n;
+}
+
 struct npgx_seqset {
+    uint64_t uid = npgx_next_uid();  // unique per set made (device caches key on it, not on the address)
     int device = 0;
     int32_t n = 0;
     std::vector<std::string> names;

@@ -2505,14 +2505,11 @@ struct npgx_aligner {
     std::vector<npgx::ScatterOp> h_ops;
     std::vector<unsigned char> h_blob;
     DevBuf<unsigned char> d_blob;
-    // async mode (AlignAsync): the re-run's jobs, list, counters, flags; the
-    // last launch's highest epoch copied back for the next call
+    // async mode (AlignAsync): the re-run's jobs, list, counters, flags
     std::vector<npgx::SaJob> h_jobs1;
     DevBuf<SaJob> d_jobs1;
     DevBuf<int32_t> d_order1, d_ctr1;
     DevBuf<uint8_t> d_retried;
-    PinnedBuf<uint32_t> h_epoch;
-    bool epoch_pending = false;
 };
 
 namespace npgx {
@@ -2523,10 +2520,7 @@ namespace npgx {
 void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, const int32_t* row_len,
                   const int32_t* job_row_start, int32_t n_jobs, AlignResult& res, const AlignAsync* as) {
     NPGX_HIP(hipSetDevice(al->device));
-    if (al->epoch_pending) {  // the last async call's highest epoch (its copy is complete: the caller synced)
-        al->epoch_base = std::max(al->epoch_base, al->h_epoch.p[0] + 1);
-        al->epoch_pending = false;
-    }
+
     auto tp = std::chrono::steady_clock::now();
     auto ms = [](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -2736,7 +2730,6 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->d_order1.ensure(std::max<size_t>(jobs.size(), 1));
         al->d_ctr1.ensure(2);
         al->d_retried.ensure(std::max<size_t>(jobs.size(), 1));
-        al->h_epoch.ensure(1);
     }
     for (int attempt = 0; attempt < 2 && !todo.empty(); attempt++) {
         DevBuf<unsigned char>& scr = attempt == 0 ? al->d_scratch : al->d_scratch2;
@@ -3414,8 +3407,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             hipLaunchKernelGGL(k_job_rows, dim3(jg), dim3(256), 0, st, al->d_jobs.p, al->d_jobs1.p, al->d_retried.p,
                                d_job_status, d_job_len, n_jobs, scr.p, al->d_scratch2.p, as->out, as->err);
             NPGX_HIP(hipGetLastError());
-            NPGX_HIP(hipMemcpyAsync(al->h_epoch.p, d_slot_epoch, 4, hipMemcpyDeviceToHost, st));
-            al->epoch_pending = true;
+            NPGX_HIP(hipMemcpyAsync(as->epoch, d_slot_epoch, 4, hipMemcpyDeviceToDevice, st));
             res.len.clear();
             res.cap.clear();
             res.bptr.clear();
@@ -3549,6 +3541,7 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
 }
 
 void aligner_timer_reset(npgx_aligner* al) { al->timer.reset(); }
+void aligner_note_epoch(npgx_aligner* al, uint32_t epoch) { al->epoch_base = std::max(al->epoch_base, epoch + 1); }
 const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al) { return al->job_stats; }
 void aligner_host_ms(npgx_aligner* al, double* prep, double* wait) {
     *prep = al->host_ms[0];

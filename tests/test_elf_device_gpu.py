@@ -112,3 +112,31 @@ def test_extend_loop_fast_device_vs_oracle(cfg, iters, monkeypatch):
     assert eng.stats()["iterations"] == o.stats()["iterations"]
     assert canon(eng.blocks()) == canon(o.blocks())
     assert eng.hash() == o.hash()
+
+
+def test_extend_loop_fast_device_host_fallback(monkeypatch):
+    """Blocks overlapping themselves (a fragment next to a shifted copy of
+    itself on the same sequence) send the device loop's OverlaplessUnion to
+    the host (SetFc's multiset mode); the result equals the host loop's and
+    the oracle's."""
+    names, seqs = synth.genome_set("small")
+    b0 = _stem_blocks(seqs, names)
+    blocks = [[f[:4] + (None,) for f in b] for b in b0]
+    for i in range(0, len(blocks), 7):
+        q, mn, mx, ori, _ = blocks[i][0]
+        if mn > 30 and mx + 30 < len(seqs[q]):
+            blocks[i].append((q, mn + 3, mx + 3, ori, None))
+    res = []
+    for dev in ("1", "0"):
+        monkeypatch.setenv("NPGX_ELF_DEVICE", dev)
+        ss, eng = _engine(seqs, names, max_iterations=4)
+        eng.set_blocks(blocks).apply("DummyAligner").apply("ExtendLoopFast")
+        res.append((canon(eng.blocks()), eng.rows_digest(), eng.stats()["iterations"],
+                    eng.stats()["counters"]["spare"]))
+    assert res[0][:3] == res[1][:3]
+    assert res[0][3] > 0  # the device loop handed OverlaplessUnion to the host
+    o = orc.BlockSetOracle(seqs, names, max_iterations=4)
+    o.set_blocks(blocks)
+    o.apply("DummyAligner")
+    o.apply("ExtendLoopFast")
+    assert canon(o.blocks()) == res[0][0]

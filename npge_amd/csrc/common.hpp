@@ -310,7 +310,8 @@ WideBufs* wide_create();
 void wide_free(WideBufs* w);
 void align_wide(WideBufs* w, hipStream_t st, const char* d_rows, const int64_t* ne_off, const int32_t* ne_len,
                 int64_t n_ne, const std::vector<WideJobIn>& in, const int params[5], int aligner_type,
-                std::vector<int32_t>& len, std::vector<int32_t>& cap, std::vector<const char*>& ptr);
+                std::vector<int32_t>& len, std::vector<int32_t>& cap, std::vector<const char*>& ptr,
+                double* wait_ms = nullptr);
 void aligner_timer_reset(npgx_aligner* al);
 const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al);
 void aligner_host_ms(npgx_aligner* al, double* prep, double* wait);  // read and clear

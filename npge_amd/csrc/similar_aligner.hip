@@ -3455,9 +3455,13 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         std::vector<int32_t> wl, wc;
         std::vector<const char*> wp;
         auto ti = al->timer.begin("align_wide", st, 0.0, 0);
+        double wide_wait = 0;  // booked as kernel wait, not host preparation
         align_wide(al->wide, st, d_rows, ne_off.data(), ne_len.data(), (int64_t)ne_len.size(), wide_in, params,
-                   o.aligner_type, wl, wc, wp);
+                   o.aligner_type, wl, wc, wp, &wide_wait);
         al->timer.end(ti, st);
+        al->host_ms[1] += wide_wait;
+        tp += std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+            std::chrono::duration<double, std::milli>(wide_wait));
         for (size_t q = 0; q < wide_idx.size(); q++) {
             res.len[wide_idx[q]] = wl[q];
             res.cap[wide_idx[q]] = wc[q];

@@ -26,6 +26,7 @@
 // A job whose output, arena or tables outgrow their first sizes is re-run
 // with larger ones (status 1); a frame stack deeper than DMAX or more than
 // MAXV gap variants is refused (NPGX_ERR_RANGE).
+#include <chrono>
 #include <cstring>
 
 #include <deque>
@@ -881,7 +882,8 @@ void wide_free(WideBufs* w) { delete w; }
 
 void align_wide(WideBufs* W, hipStream_t st, const char* d_rows, const int64_t* ne_off, const int32_t* ne_len,
                 int64_t n_ne, const std::vector<WideJobIn>& in, const int params[5], int aligner_type,
-                std::vector<int32_t>& len, std::vector<int32_t>& cap, std::vector<const char*>& ptr) {
+                std::vector<int32_t>& len, std::vector<int32_t>& cap, std::vector<const char*>& ptr,
+                double* wait_ms) {
     using namespace wide;
     const size_t nj = in.size();
     len.assign(nj, 0);
@@ -1012,9 +1014,13 @@ void align_wide(WideBufs* W, hipStream_t st, const char* d_rows, const int64_t* 
             hipLaunchKernelGGL(k_align_wide, dim3((unsigned)nw), dim3(WT), 0, st, A);
             NPGX_HIP(hipGetLastError());
             std::vector<int32_t> L(nw), S(nw);
-            NPGX_HIP(hipMemcpyAsync(L.data(), W->len.p, nw * 4, hipMemcpyDeviceToHost, st));
-            NPGX_HIP(hipMemcpyAsync(S.data(), W->status.p, nw * 4, hipMemcpyDeviceToHost, st));
+            // (the wait for the launch: the copies into pageable memory wait too)
+            const auto tw = std::chrono::steady_clock::now();
             NPGX_HIP(stream_wait(st));
+            NPGX_HIP(hipMemcpy(L.data(), W->len.p, nw * 4, hipMemcpyDeviceToHost));
+            NPGX_HIP(hipMemcpy(S.data(), W->status.p, nw * 4, hipMemcpyDeviceToHost));
+            if (wait_ms)
+                *wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
             for (size_t t = w0; t < w1; t++) {
                 NPGX_REQUIRE(S[t - w0] != 2, NPGX_ERR_RANGE,
                              "wide alignment: more than 96 nested re-alignments or 8 gap variants");

@@ -82,11 +82,43 @@ def test_ou_device_many_sequences():
 def _draft(cfg, device, monkeypatch):
     from npge_amd.anchor_finder import AnchorFinder
     monkeypatch.setenv("NPGX_ELF_DEVICE", "1" if device else "0")
+    monkeypatch.setenv("NPGX_ELF_CHECK", "1")  # a bad table or flank plan fails loudly instead of faulting
     names, seqs = synth.genome_set(cfg)
     ss, eng = _engine(seqs, names)
     eng.apply("DraftPangenome", af=AnchorFinder())
     st = eng.stats()
     return eng.blocks(), eng.rows_digest(), st
+
+
+def test_ou_device_multi_launch_passes(monkeypatch):
+    """The table passes as count / device-wide scan / fill launches (tables of
+    more than 8192 blocks take them; NPGX_ELF_PASS_WG=0 forces them here)."""
+    monkeypatch.setenv("NPGX_ELF_PASS_WG", "0")
+    rng = np.random.default_rng(31)
+    n_seqs, seq_len = 6, 300000
+    seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
+    names = ["m%d&c&c" % i for i in range(n_seqs)]
+    blocks = _ou_blocks(rng, n_seqs, seq_len, 1200, 400, False)
+    ss, eng = _engine(seqs, names)
+    o = orc.BlockSetOracle(seqs, names)
+    eng.set_blocks(blocks).apply("OverlaplessUnion@device")
+    o.set_blocks(blocks)
+    o.apply("OverlaplessUnion")
+    assert eng.blocks() == o.blocks()
+
+
+@pytest.mark.parametrize("cfg,only", [("tiny", p) for p in ("plan", "stitch", "fix_ends_plan", "slice", "ou_prep",
+                                                              "ou_scan", "ou_compact")]
+                         + [("tiny", ""), ("rtiny", "")])
+def test_draft_device_multi_launch_passes(cfg, only, monkeypatch):
+    """Every table pass (or one, `only`) in the count / scan / fill form."""
+    monkeypatch.setenv("NPGX_ELF_PASS_WG", "0")
+    monkeypatch.setenv("NPGX_ELF_PASS_MULTI", only)
+    b_dev, d_dev, s_dev = _draft(cfg, True, monkeypatch)
+    b_host, d_host, s_host = _draft(cfg, False, monkeypatch)
+    assert canon(b_dev) == canon(b_host)
+    assert d_dev == d_host
+    assert s_dev["iterations"] == s_host["iterations"]
 
 
 @pytest.mark.parametrize("cfg", ["tiny", "small", "rtiny", "rsmall"])
@@ -102,6 +134,7 @@ def test_draft_device_equals_host_loop(cfg, monkeypatch):
 @pytest.mark.parametrize("cfg,iters", [("tiny", 10), ("small", 2), ("rtiny", 10)])
 def test_extend_loop_fast_device_vs_oracle(cfg, iters, monkeypatch):
     monkeypatch.setenv("NPGX_ELF_DEVICE", "1")
+    monkeypatch.setenv("NPGX_ELF_CHECK", "1")
     names, seqs = synth.genome_set(cfg)
     b0 = _stem_blocks(seqs, names)
     ss, eng = _engine(seqs, names, max_iterations=iters)

@@ -44,5 +44,16 @@ else
     step pmc_$c
     timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/c3_$c -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/pmc_$c.log 2>&1 || { tail -5 $O/pmc_$c.log; exit 1; }
   done
+  cd $R
+  step bench_pairs
+  timeout -k 10 400 python bench.py --mode pairs --config C4 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_pairs.log 2>&1 || { tail -5 $O/bench_pairs.log; exit 1; }
+  tail -1 $O/bench_pairs.log | cut -c1-200
+  cd /tmp
+  step rocprof_pairs
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_pairs -o run -- python3 $R/bench.py --mode pairs --config C4 --pairs 32 --steps 1 --warmup 1 --no-cpu-baseline > $O/prof_pairs.log 2>&1 || { tail -5 $O/prof_pairs.log; exit 1; }
+  for c in FETCH_SIZE WRITE_SIZE; do
+    step pmc_pairs_$c
+    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pairs_$c -o run -- python3 $R/bench.py --mode pairs --config C4 --pairs 32 --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_pairs_$c.log 2>&1 || { tail -5 $O/pmc_pairs_$c.log; exit 1; }
+  done
 fi
 step done

@@ -2456,7 +2456,7 @@ struct npgx_aligner {
     // then whole prefixes from `long_m` shifts on (find_word_long,
     // sa_device.hpp; NPGX_LONG_HEAD / NPGX_LONG_M; long_head 0: incremental
     // only, the round-4 search)
-    int long_head = 32;
+    int long_head = 128;
     int long_m = 512;
     // twins of the split jobs (NPGX_TWINS: 0 never -- the default: measured at
     // C3 and C5 the whole-job bad region they serve is rare among split jobs

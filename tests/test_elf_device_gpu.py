@@ -92,7 +92,7 @@ def _draft(cfg, device, monkeypatch):
 
 def test_ou_device_multi_launch_passes(monkeypatch):
     """The table passes as count / device-wide scan / fill launches (tables of
-    more than 8192 blocks take them; NPGX_ELF_PASS_WG=0 forces them here)."""
+    more than 2048 blocks take them; NPGX_ELF_PASS_WG=0 forces them here)."""
     monkeypatch.setenv("NPGX_ELF_PASS_WG", "0")
     rng = np.random.default_rng(31)
     n_seqs, seq_len = 6, 300000

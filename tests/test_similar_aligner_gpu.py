@@ -353,7 +353,7 @@ def _restart_family(rng, n, core, ins, d=0.01, repeat=0.0):
     return rows
 
 
-@pytest.mark.parametrize("head,m", [("32", "512"), ("0", "512"), ("1", "64"), ("64", "2048")])
+@pytest.mark.parametrize("head,m", [("128", "512"), ("32", "512"), ("0", "512"), ("1", "64"), ("64", "2048")])
 def test_long_restart_searches(head, m, monkeypatch):
     """try_aligned's prefix search (find_word_long, sa_device.hpp) against the
     oracle's find_best_word loop: unrelated insertions of up to 6000 bases

@@ -365,6 +365,17 @@ int npgx_blockset_create(const npgx_seqset* s, const npgx_bb_options* o, npgx_bl
  * worker thread.  No reference counterpart: a device-memory sharing hint. */
 int npgx_blockset_create_sharing(const npgx_seqset* s, const npgx_bb_options* o, npgx_blockset* lender,
                                  npgx_blockset** out);
+/* tuning hooks with no reference counterpart (results never change):
+ *   "long-head"  the set's aligner searches that many shifts incrementally
+ *                before the prefix search (default 128); 0 = incremental only,
+ *                and the aligner then launches its kernels without the prefix
+ *                search's call (less scratch: the form for many concurrent
+ *                streams, e.g. the pair job).  Sets sharing the aligner share it.
+ *   "elf-device" ExtendLoopFast on the device (1), on the host (0) or the
+ *                default (-1, the device where its rules allow); sets made by
+ *                npgx_blockset_create_sharing inherit the lender's.
+ * NPGX_ERR_ARG for an unknown key or a value out of range. */
+int npgx_blockset_tune(npgx_blockset* b, const char* key, int64_t value);
 /* replace the blocks; row_off == NULL: no rows, else row i = rows[row_off[i]..row_off[i+1])
  * (a block whose rows are all empty is unaligned) */
 int npgx_blockset_set_blocks(npgx_blockset* b, int64_t n_blocks, const int64_t* block_start,

@@ -219,6 +219,14 @@ class BlockSetEngine:
         _capi.check(L.npgx_blockset_deconseq(self._h, src._h, cons._h))
         return self
 
+    def tune(self, key, value):
+        """npgx_blockset_tune: "long-head" (the aligner's incremental shifts
+        before the prefix search; 0 = never, the low-scratch kernels) or
+        "elf-device" (1 / 0 / -1: ExtendLoopFast on the device / host /
+        default).  Results do not change."""
+        _capi.check(_capi.lib().npgx_blockset_tune(self._h, key.encode(), ctypes.c_int64(int(value))))
+        return self
+
     def hash(self):
         h = ctypes.c_uint64()
         _capi.check(_capi.lib().npgx_blockset_hash(self._h, ctypes.byref(h)))

@@ -1093,8 +1093,9 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
 
         // --- pass 2a: FoundFragment counts per hash
         ti = af->timer.begin("ff_count", st, local_windows * (0.375 + 12.0), local_windows);
-        // NPGX_AF_SLOT_COUNT=0: the counts by atomics on counts[] (the round-4 form)
-        static const bool slot_count = !(getenv("NPGX_AF_SLOT_COUNT") && getenv("NPGX_AF_SLOT_COUNT")[0] == '0');
+        // the counts by atomics on counts[] (NPGX_AF_SLOT_COUNT=1: the counts in the membership table's slots; measured no faster at C3 / C5,
+        // profiles/r05j_af_slot_counts.txt)
+        static const bool slot_count = getenv("NPGX_AF_SLOT_COUNT") && getenv("NPGX_AF_SLOT_COUNT")[0] == '1';
         if (run_local) {
             hipLaunchKernelGGL(k_ff_count, grid, block, 0, st, A, T, slot_count ? nullptr : af->counts.p);
             if (slot_count)

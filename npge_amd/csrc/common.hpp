@@ -297,6 +297,8 @@ struct AlignAsync {
 // the highest word-table epoch an async call reached (read from AlignAsync::epoch
 // after the caller's wait): the next call's tables start above it
 void aligner_note_epoch(npgx_aligner* al, uint32_t epoch);
+void aligner_set_long_head(npgx_aligner* al, int32_t long_head);
+int32_t aligner_long_head(const npgx_aligner* al);
 void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, const int32_t* row_len,
                   const int32_t* job_row_start, int32_t n_jobs, AlignResult& res, const AlignAsync* as = nullptr);
 // wide_aligner.hip: align_seqs for problems of more than 64 non-empty rows (one

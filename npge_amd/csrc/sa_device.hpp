@@ -544,7 +544,12 @@ __device__ __forceinline__ void lw_words(const LdsU8* buf, int lane, int ac, uns
     }
 }
 
-__device__ __noinline__ LongOut find_word_long(const char* vp, int vlen, int vd, int pos, int lane, int n, int ac,
+#ifdef SA_LONG_INLINE  // (A/B builds: inlined instead of called)
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+LongOut find_word_long(const char* vp, int vlen, int vd, int pos, int lane, int n, int ac,
                                                int max_shift, int M0, unsigned long long* W,
                                                unsigned long long* tkeys, unsigned long long* tmask,
                                                uint32_t tcap_log2, uint32_t epoch) {
@@ -740,7 +745,14 @@ __device__ __noinline__ LongOut find_word_long(const char* vp, int vlen, int vd,
 
 
 // ---------------------------------------------------------------- process_seqs
-struct Proc {
+// LONG: try_aligned may switch to the prefix search (find_word_long).  Its
+// call costs the kernels that can make it 664 bytes of scratch a lane against
+// 312 (the registers live across the call): under many concurrent streams
+// (the pair job) that scratch throttled the aligner by a fifth, so the
+// kernels come in both forms and an aligner with long_head 0 launches the
+// ones without the call.
+template <bool LONG>
+struct ProcT {
     WaveCtx w;
     Params P;
     Slot S;
@@ -750,6 +762,7 @@ struct Proc {
     int pos;         // this lane's cursor
     int col;         // output cursor (all rows equal length between steps)
     bool ovf;
+    bool rovf;       // ... because the output room ran out (not a table or the stack)
     uint32_t epoch;   // global word-table epoch (carried from one Proc to the next)
     uint32_t lepoch;  // LDS word-table epoch
     int n_aligned_calls, n_shifts, n_gaps, n_fast;
@@ -769,9 +782,9 @@ struct Proc {
     long long prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
-    __device__ __forceinline__ Proc(const WaveCtx& w_, const Params& P_, const Slot& S_, char* ob_, int cap_,
+    __device__ __forceinline__ ProcT(const WaveCtx& w_, const Params& P_, const Slot& S_, char* ob_, int cap_,
                                     uint32_t ep, uint32_t lep)
-        : w(w_), P(P_), S(S_), ob(ob_), cap(cap_), pos(0), col(0), ovf(false), epoch(ep), lepoch(lep),
+        : w(w_), P(P_), S(S_), ob(ob_), cap(cap_), pos(0), col(0), ovf(false), rovf(false), epoch(ep), lepoch(lep),
           n_aligned_calls(0), n_shifts(0), n_gaps(0), n_fast(0), tg(nullptr), tK(0), tm(0), tv(0), tbase(0),
           chk(false), stop(false) {}
 
@@ -805,7 +818,7 @@ struct Proc {
 
     __device__ __forceinline__ void put(int c, char x) {
         if (c < cap) ob[(size_t)w.lane * cap + c] = x;
-        else ovf = true;
+        else ovf = rovf = true;
     }
     __device__ __forceinline__ int ch(int q) const { return vch(v, q, w.lane); }
     __device__ __forceinline__ bool is_stop(int shift) const { return any_lane(w, pos + shift >= v.len); }
@@ -831,7 +844,7 @@ struct Proc {
     // append_gaps :79-89 is the padding.  Advances pos by t and col by m.
     __device__ __forceinline__ void write_tails(int t, int m) {
         if (col + m > cap) {
-            ovf = true;
+            ovf = rovf = true;
             return;
         }
         __syncthreads();
@@ -1028,7 +1041,7 @@ struct Proc {
         n_aligned_calls++;
         // the first P.lh shifts incrementally (most searches end there), then
         // whole prefixes (find_word_long)
-        const bool lng = P.lh > 0 && w.n >= 2 && max_shift > P.lh;
+        const bool lng = LONG && P.lh > 0 && w.n >= 2 && max_shift > P.lh;
         const int head = lng ? P.lh : max_shift;
         if (w.n <= VEC_ROWS) {
             const VecOut r = find_word_vec(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, head, S.lwords, S.tkeys,
@@ -1388,7 +1401,7 @@ struct Proc {
             v.d = (l & (int)0x80000000) ? -1 : 1;
             pos = S.st_pos[o];
             if (col > cap) {
-                ovf = true;
+                ovf = rovf = true;
             } else {
                 __syncthreads();
                 cm_reverse(w, ob, cap, c0, col);

@@ -860,7 +860,8 @@ __device__ __forceinline__ bool tail_identical(const WaveCtx& w, const char* B, 
 
 // realing_end (:461-484) on B; returns the length (remove_gaps has nothing to
 // remove from the similar aligner's columns, see k_align_jobs)
-__device__ int finish_tail(Proc& pr, const WaveCtx& w, char* B, char* C, int cap, int L, char* stage,
+template <class PR>
+__device__ int finish_tail(PR& pr, const WaveCtx& w, char* B, char* C, int cap, int L, char* stage,
                            int stage_bytes, int ac, bool& ovf) {
     pr.ob = B;
     int prefix = L - ac;
@@ -892,6 +893,7 @@ __device__ __forceinline__ int fin_width(const SaArgs& a, int4 rg) {
 // k_align_sub: every bad region of every deferred job, one wave each; with a
 // plan (k_plan_subs) the segments of the split sub-jobs first, then the other
 // sub-jobs
+template <bool LONG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER_EU))) void k_align_sub(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
@@ -936,8 +938,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
             v.len = ((const int*)(a.pool + d.out_off))[lane] - start;
         }
         char* out = seg ? (char*)(a.seg_pool + sg.out) : (char*)(a.pool + d.out_off + 256);
+        int ocap = d.out_cap;  // (a re-run below moves the output)
         const unsigned long long w_start = wall_clock64();
-        Proc pr(w, a.P, e.S, out, seg ? sg.cap : d.out_cap, epoch, lepoch);
+        ProcT<LONG> pr(w, a.P, e.S, out, seg ? sg.cap : d.out_cap, epoch, lepoch);
         int Lc = 0;
         bool ovf = false;
         if (!idle) {
@@ -947,6 +950,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
             ovf = any_lane(w, pr.ovf);
         }
         __syncthreads();
+        // a bad region whose re-alignment outgrew 2 x width + 64 columns (rows
+        // with unrelated insertions: R3): again at once in a room of its rows'
+        // total length (the proven bound) from the pool, instead of the whole
+        // job re-running at attempt 1
+        if (!seg && !idle && ovf && any_lane(w, pr.rovf) && !any_lane(w, pr.ovf && !pr.rovf)) {
+            const int tot = wave_sum(w.act ? v.len : 0);
+            const int room = min(cap, (tot + 15) & ~15);
+            long long off2 = -1;
+            if (room > d.out_cap) {
+                if (lane == 0) off2 = reserve(&a.alloc[0], (unsigned long long)sub_bytes(n, room),
+                                              (unsigned long long)a.pool_cap);
+                off2 = (long long)bcast64((unsigned long long)off2, 0);
+            }
+            if (off2 >= 0) {
+                if (w.act) ((int*)(a.pool + off2))[lane] = ((const int*)(a.pool + d.out_off))[lane];
+                if (lane == 0) {
+                    SaSub d2 = d;
+                    d2.out_off = off2;
+                    d2.out_cap = room;
+                    a.subs[sn] = d2;
+                }
+                out = (char*)(a.pool + off2 + 256);
+                ocap = room;
+                ProcT<LONG> pr2(w, a.P, e.S, out, room, pr.epoch, pr.lepoch);
+                Lc = pr2.run(v, 0);
+                ovf = any_lane(w, pr2.ovf);
+                pr.epoch = pr2.epoch;
+                pr.lepoch = pr2.lepoch;
+                if (lane == 0 && a.counters) atomicAdd(&a.counters[3], 1u);  // (sub-jobs re-run)
+            }
+            __syncthreads();
+        }
         if (lane == 0 && a.job_stats) {  // (statistics wanted: the critical path of the launch)
             int64_t* wl = seg ? a.seg_wall + 2 * (size_t)seg_t : (a.sub_wall ? a.sub_wall + 2 * (size_t)sn : nullptr);
             if (wl) {
@@ -959,7 +994,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
                 a.seg_res[seg_t] = idle ? make_int4(-1, 0, 0, 0)
                                         : make_int4(pr.stop ? pr.tm + 1 : sp.K, Lc, ovf ? 1 : 0, 0);
         } else {
-            const int after = ovf ? 0 : count_equal_cols(w, out, d.out_cap, 0, Lc, nullptr);
+            const int after = ovf ? 0 : count_equal_cols(w, out, ocap, 0, Lc, nullptr);
             if (lane == 0) a.sub_res[sn] = make_int2(ovf ? -1 : Lc, after);
         }
         epoch = pr.epoch;
@@ -971,6 +1006,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
 
 // k_align_finish: realing_end on the deferred jobs' B (= good regions of A +
 // the better of each bad region and its re-alignment, k_fin_copy)
+template <bool LONG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_align_finish(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
@@ -1004,10 +1040,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
         colB = wave_sum(colB);
         bool ovf = ballot(bad) != 0 || colB > cap;
-        Proc pr(w, a.P, e.S, B, cap, epoch, lepoch);
+        // an overflowed job's length field holds why (negative; NPGX_RETRY_DEBUG)
+        const int why = ballot(bad) != 0 ? -10 : colB > cap ? -11 : -12;
+        ProcT<LONG> pr(w, a.P, e.S, B, cap, epoch, lepoch);
         const int L = finish_tail(pr, w, B, C, cap, colB, e.stage, a.stage_bytes, a.P.ac, ovf);
         if (lane == 0) {
-            a.job_len[j] = ovf ? 0 : L;
+            a.job_len[j] = ovf ? why : L;
             a.job_status[j] = ovf ? 1 : 0;
         }
         epoch = pr.epoch;
@@ -1061,10 +1099,10 @@ __host__ __device__ __forceinline__ int split_len_for(int split, int n) {
 // room for a walk that misses up to about eight sync states in a row (the
 // speculation then still chains; past that its job re-runs whole), never
 // more than the suffix bound or `limit`
-__host__ __device__ __forceinline__ int seg_cap_for(int mx, int k, int K, int win, int64_t limit) {
+__host__ __device__ __forceinline__ int seg_cap_for(int mx, int k, int K, int win, int64_t limit, bool full = false) {
     const int64_t rest = mx - (int64_t)mx * k / K + win;
     const int64_t reach = 8ll * (mx / K + 1) + 2ll * win;
-    const int64_t lim = rest < reach ? rest : reach;
+    const int64_t lim = (full || rest < reach) ? rest : reach;  // full: the rest of the longest row, twice
     const int64_t c = (2 * lim + 64 + 15) & ~15ll;
     return (int)(c < limit ? c : limit);
 }
@@ -1474,7 +1512,7 @@ __global__ __launch_bounds__(POST_THREADS) void k_split_chain(SaArgs a) {
         while (k < sp.K) {
             const int nxt = nx[k], cols = nc[k];
             if (nxt <= k || cols < 0 || col + cols > job.cap) {  // (an idle segment is never on the chain)
-                fail = 1;
+                fail = nxt <= k ? 1 : cols < 0 ? 2 : 3;  // (NPGX_RETRY_DEBUG: job_len -201 / -202 / -203)
                 break;
             }
             ch[np] = make_int4(sp.seg0 + k, cols, col, 0);
@@ -1602,7 +1640,7 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
     const int L0 = ps.L0, nw = (L0 + 63) >> 6;
     if (ps.fail || (long long)nw * 16 > area_bytes) {
         if (tid == 0) {
-            a.job_len[j] = 0;
+            a.job_len[j] = ps.fail ? -(200 + ps.fail) : -21;
             a.job_status[j] = 1;
         }
         return;
@@ -1611,7 +1649,7 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
     const int R = regions_block<G, I>(gm, nw, L0, a.P.wf, a.P.min_length, area_bytes, jr, job.reg_cap, ps.scan);
     if (R < 0 || R > job.reg_cap) {
         if (tid == 0) {
-            a.job_len[j] = 0;
+            a.job_len[j] = -22;
             a.job_status[j] = 1;
         }
         return;
@@ -1685,7 +1723,7 @@ __device__ void split_post_body(const SaArgs& a, const SaSplit& sp, G* gm, long 
     __syncthreads();
     if (ps.R < 0) {  // sub-job pool full
         if (tid == 0) {
-            a.job_len[j] = 0;
+            a.job_len[j] = -23;
             a.job_status[j] = 1;
         }
         return;
@@ -1979,6 +2017,7 @@ __global__ __launch_bounds__(POST_THREADS) void k_fin_copy(SaArgs a, int lds_int
     }
 }
 
+template <bool LONG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER_EU))) void k_align_jobs(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
@@ -2119,7 +2158,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         } else {
             // 1. process_seqs
             // one Proc for every process_seqs call of the job (state is per call)
-            Proc pr(w, a.P, S, chained ? (char*)(a.seg_pool + sg.out) : A, chained ? sg.cap : cap, epoch, lepoch);
+            ProcT<LONG> pr(w, a.P, S, chained ? (char*)(a.seg_pool + sg.out) : A, chained ? sg.cap : cap, epoch, lepoch);
             long long t0 = clock64();
             int L0 = 0;
             if (!idle) {
@@ -2274,7 +2313,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
             __syncthreads();
         }
         if (lane == 0) {
-            a.job_len[j] = ovf ? 0 : L;
+            a.job_len[j] = ovf ? -30 : L;
             a.job_status[j] = ovf ? 1 : deferred ? 3 : (B == A ? 2 : 0);  // 2: the rows are in A, 3: deferred
         }
         if (lane == 0 && a.job_stats) {  // only when the statistics are wanted
@@ -2458,6 +2497,9 @@ struct npgx_aligner {
     // only, the round-4 search)
     int long_head = 128;
     int long_m = 512;
+    // split jobs whose segment rooms for the whole row suffixes take at most
+    // this many bytes get them (NPGX_SEG_FULL_MB; 0: the 8-sync-state rooms)
+    int64_t seg_full_bytes = 64ll << 20;
     // twins of the split jobs (NPGX_TWINS: 0 never -- the default: measured at
     // C3 and C5 the whole-job bad region they serve is rare among split jobs
     // and their segments slow the launch -- 1 always, -1 in launches with few
@@ -2731,8 +2773,18 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->d_ctr1.ensure(2);
         al->d_retried.ensure(std::max<size_t>(jobs.size(), 1));
     }
+    // NPGX_RETRY_DEBUG: the re-run jobs (rows, longest row, residues, first
+    // room, split or not, final length) to stderr
+    static const bool rdbg = getenv("NPGX_RETRY_DEBUG") != nullptr;
+    std::vector<int32_t> dbg_cap0;
+    std::vector<uint8_t> dbg_split;
+    std::vector<int32_t> dbg_why;  // attempt 0's overflow reason (-job_len)
     for (int attempt = 0; attempt < 2 && !todo.empty(); attempt++) {
         DevBuf<unsigned char>& scr = attempt == 0 ? al->d_scratch : al->d_scratch2;
+        if (attempt == 1 && rdbg) {
+            dbg_cap0.assign(n_jobs, 0);
+            for (int32_t j : todo) dbg_cap0[j] = jobs[j].cap;
+        }
         if (attempt == 1) {  // re-run overflowed jobs at the proven bound, in a second scratch
             scratch = 0;
             max_cap = 1;
@@ -2792,11 +2844,18 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                     part0.push_back(part0.back() + (J.cap + CHAIN_PART - 1) / CHAIN_PART);
                 }
                 n_tgt += (int64_t)(K - 1) * J.n;
+                // rooms for the whole rest of the rows when that stays within
+                // seg_full_bytes for the job: a walk that misses the later
+                // sync states (repeat insertions: R3) then still finishes its
+                // segment instead of overflowing and re-running the job whole
+                int64_t full_bytes = 0;
+                for (int k = 0; k < K; k++) full_bytes += (int64_t)J.n * seg_cap_for(mx, k, K, sp.win, J.cap, true);
+                const bool full = full_bytes <= al->seg_full_bytes;
                 for (int k = 0; k < K; k++) {
                     SaSeg g;
                     g.split = (int32_t)splits.size();
                     g.k = k;
-                    g.cap = seg_cap_for(mx, k, K, sp.win, J.cap);
+                    g.cap = seg_cap_for(mx, k, K, sp.win, J.cap, full);
                     g.pad = 0;
                     g.out = seg_bytes;
                     seg_bytes += ((int64_t)J.n * g.cap + 255) & ~255ll;
@@ -2860,6 +2919,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 splits[si].twin = ti + 1;
                 splits.push_back(tw);
             }
+        }
+        if (rdbg && attempt == 0) {
+            dbg_split.assign(n_jobs, 0);
+            for (const SaSplit& sp : splits) dbg_split[sp.job] = 1;
         }
         if (splits.empty()) {
             queue = todo;
@@ -3156,7 +3219,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         flush();
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
                                     double(residues) * 2.0, residues);
-        hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+        if (al->long_head > 0) hipLaunchKernelGGL(k_align_jobs<true>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+        else hipLaunchKernelGGL(k_align_jobs<false>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
         pmark(7);
@@ -3212,7 +3276,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 al->timer.end(ti, st);
             }
             ti = al->timer.begin("align_sub", st, 0.0, 0);
-            hipLaunchKernelGGL(k_align_sub, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+            if (al->long_head > 0) hipLaunchKernelGGL(k_align_sub<true>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+            else hipLaunchKernelGGL(k_align_sub<false>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
             if (split_subs) {  // the split sub-jobs' chains
@@ -3231,7 +3296,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 al->timer.end(ti, st);
             }
             ti = al->timer.begin("align_finish", st, 0.0, 0);
-            hipLaunchKernelGGL(k_align_finish, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+            if (al->long_head > 0) hipLaunchKernelGGL(k_align_finish<true>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+            else hipLaunchKernelGGL(k_align_finish<false>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
         }
@@ -3402,7 +3468,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A1.cap_splits = A1.cap_segs = 0;
             A1.cap_tgt = A1.cap_find = A1.cap_pool = 0;
             size_t tr = al->timer.begin("align_jobs_retry", st, 0.0, 0);
-            hipLaunchKernelGGL(k_align_jobs, dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
+            if (al->long_head > 0) hipLaunchKernelGGL(k_align_jobs<true>, dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
+            else hipLaunchKernelGGL(k_align_jobs<false>, dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
             al->timer.end(tr, st);
             hipLaunchKernelGGL(k_job_rows, dim3(jg), dim3(256), 0, st, al->d_jobs.p, al->d_jobs1.p, al->d_retried.p,
                                d_job_status, d_job_len, n_jobs, scr.p, al->d_scratch2.p, as->out, as->err);
@@ -3435,6 +3502,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             NPGX_REQUIRE(jstat[j] >= 0 && jstat[j] <= 2, NPGX_ERR_STATE, "alignment job left unfinished");
             if (jstat[j] == 1) {
                 again.push_back(j);
+                if (rdbg && attempt == 0) {
+                    dbg_why.resize(n_jobs, 0);
+                    dbg_why[j] = jlen[j];
+                }
                 continue;
             }
             if (al->want_stats)
@@ -3447,6 +3518,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         }
         if (attempt == 1 && !again.empty())
             throw Error(NPGX_ERR_RANGE, "alignment exceeded the proven column bound");
+        if (attempt == 1 && rdbg)
+            for (int32_t j : todo)
+                fprintf(stderr, "retry job %d: rows %d longest %d residues %d room0 %d split %d length %d why %d\n", j,
+                        jobs[j].n, jmax[j], jsum[j], dbg_cap0[j], j < (int32_t)dbg_split.size() ? dbg_split[j] : -1,
+                        jlen[j], j < (int32_t)dbg_why.size() ? -dbg_why[j] : 0);
         todo.swap(again);
     }
     if (!wide_idx.empty()) {
@@ -3546,6 +3622,8 @@ void align_batch(npgx_aligner* al, const char* rows, const int64_t* row_off,
 
 void aligner_timer_reset(npgx_aligner* al) { al->timer.reset(); }
 void aligner_note_epoch(npgx_aligner* al, uint32_t epoch) { al->epoch_base = std::max(al->epoch_base, epoch + 1); }
+void aligner_set_long_head(npgx_aligner* al, int32_t long_head) { al->long_head = std::max(0, long_head); }
+int32_t aligner_long_head(const npgx_aligner* al) { return al->long_head; }
 const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al) { return al->job_stats; }
 void aligner_host_ms(npgx_aligner* al, double* prep, double* wait) {
     *prep = al->host_ms[0];
@@ -3599,6 +3677,8 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         if (lh && *lh) a->long_head = std::max(0, atoi(lh));
         const char* lm = getenv("NPGX_LONG_M");
         if (lm && *lm) a->long_m = std::max(64, atoi(lm));
+        const char* sf = getenv("NPGX_SEG_FULL_MB");
+        if (sf && *sf) a->seg_full_bytes = (int64_t)std::max(0, atoi(sf)) << 20;
         const char* tw = getenv("NPGX_TWINS");
         if (tw && *tw) a->twins = atoi(tw) > 0 ? 1 : (atoi(tw) == 0 ? 0 : -1);
         const char* sb = getenv("NPGX_SLOT_BUDGET_MB");
@@ -3613,10 +3693,11 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         }
         // dynamic LDS of each kernel at most (k_split_post and k_fin_copy also
         // have static LDS)
-        const std::pair<const void*, int> kernels[5] = {
-            {(const void*)k_align_jobs, (int)LDS_PER_CU}, {(const void*)k_align_sub, (int)LDS_PER_CU},
-            {(const void*)k_align_finish, (int)LDS_PER_CU}, {(const void*)k_split_post, (int)POST_LDS},
-            {(const void*)k_fin_copy, 32768 * 4}};
+        const std::pair<const void*, int> kernels[8] = {
+            {(const void*)k_align_jobs<true>, (int)LDS_PER_CU},   {(const void*)k_align_sub<true>, (int)LDS_PER_CU},
+            {(const void*)k_align_finish<true>, (int)LDS_PER_CU}, {(const void*)k_align_jobs<false>, (int)LDS_PER_CU},
+            {(const void*)k_align_sub<false>, (int)LDS_PER_CU},   {(const void*)k_align_finish<false>, (int)LDS_PER_CU},
+            {(const void*)k_split_post, (int)POST_LDS},          {(const void*)k_fin_copy, 32768 * 4}};
         bool lds_ok = true;
         for (const auto& k : kernels)
             lds_ok = lds_ok && hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, k.second) ==

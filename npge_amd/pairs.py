@@ -24,6 +24,7 @@ npgx_comm) use no GPU call and are tested on CPU with gloo
 """
 import ctypes
 import itertools
+import os
 import threading
 import time
 
@@ -126,6 +127,21 @@ def gather_u64(comm, arr, device=None):
     return out, list(counts)
 
 
+# npgx_blockset_tune settings of the pair workers (results do not change).
+# Many concurrent streams: the aligner kernels without the prefix search's call
+# (its scratch throttled them by a fifth, gpurun_out r05n / profiles), and
+# ExtendLoopFast on the host, whose bookkeeping spreads over the workers' cores
+# while the device loop's many small kernels queue behind the other workers'
+PAIR_TUNING = {"long-head": 0, "elf-device": 0}
+
+
+def pair_tuning():
+    """PAIR_TUNING, or the JSON object in NPGX_PAIR_TUNING (A/B runs)."""
+    import json
+    e = os.environ.get("NPGX_PAIR_TUNING")
+    return dict(json.loads(e)) if e else dict(PAIR_TUNING)
+
+
 class PairJobs:
     """The rank's share of the pair-sharded job: its pairs resident in HBM (one
     sequence set + block set + AnchorFinder handle per pair, made before any
@@ -133,7 +149,7 @@ class PairJobs:
     plus the final gather."""
 
     def __init__(self, names, seqs, rank=0, world=1, comm=None, workers=4, pairs=None, device=0,
-                 gather_device=None):
+                 gather_device=None, tuning=None):
         from . import _capi
         from .pipeline import BlockBuild
         self.pairs = all_pairs(names) if pairs is None else list(pairs)
@@ -158,7 +174,11 @@ class PairJobs:
             w = self.owner[k]
             lender = self.jobs[first[w]][2] if w in first else None
             first.setdefault(w, k)
-            self.jobs.append((p, ss, BlockBuild(ss, pn, ps, lender=lender)))
+            bb = BlockBuild(ss, pn, ps, lender=lender)
+            if lender is None:  # the worker's aligner (shared by its pairs) and the mode its pairs inherit
+                for key, value in (pair_tuning() if tuning is None else tuning).items():
+                    bb.eng.tune(key, value)
+            self.jobs.append((p, ss, bb))
         self.ktimes = [None] * len(self.jobs)
         self.records = None
         self.summary = None

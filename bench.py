@@ -466,7 +466,7 @@ def pmc_traffic(kernel, config):
         return {"traffic": None}
     doc = json.load(open(files[-1]))
     for name, v in doc["kernels"].items():
-        if name.split("::")[-1] == "k_" + kernel:
+        if name.split("::")[-1].split("<")[0] == "k_" + kernel:  # (k_align_jobs<true>: the kernel's forms)
             return {"traffic": v["traffic_bytes_per_launch"], "traffic_source": os.path.basename(files[-1]),
                     "traffic_fetch": v["fetch_bytes_per_launch"], "traffic_write": v["write_bytes_per_launch"]}
     return {"traffic": None}

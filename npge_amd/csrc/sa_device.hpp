@@ -71,8 +71,8 @@ struct Slot {
 };
 
 static constexpr int VEC_ROWS = 8;
-#ifndef SA_FAST_ROWS
-#define SA_FAST_ROWS 4
+#ifndef SA_FAST_ROWS  // (4 measured no faster at C3 / R3 / C2 and 2 % slower on the pair job, r05e / r05n)
+#define SA_FAST_ROWS 1
 #endif
 static constexpr int FR = SA_FAST_ROWS;  // fast_run: rows loaded per batch
 typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // LDS-qualified word-table entry

@@ -90,10 +90,13 @@ def _draft(cfg, device, monkeypatch):
     return eng.blocks(), eng.rows_digest(), st
 
 
-def test_ou_device_multi_launch_passes(monkeypatch):
-    """The table passes as count / device-wide scan / fill launches (tables of
-    more than 2048 blocks take them; NPGX_ELF_PASS_WG=0 forces them here)."""
+@pytest.mark.parametrize("scan", ["0", "1"])
+def test_ou_device_multi_launch_passes(scan, monkeypatch):
+    """The table passes in their many-workgroup forms (tables of more than
+    2048 blocks take them; NPGX_ELF_PASS_WG=0 forces them here): the look-back
+    launch, or (scan=1) count / device-wide scan / fill launches."""
     monkeypatch.setenv("NPGX_ELF_PASS_WG", "0")
+    monkeypatch.setenv("NPGX_ELF_PASS_SCAN", scan)
     rng = np.random.default_rng(31)
     n_seqs, seq_len = 6, 300000
     seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
@@ -107,13 +110,16 @@ def test_ou_device_multi_launch_passes(monkeypatch):
     assert eng.blocks() == o.blocks()
 
 
-@pytest.mark.parametrize("cfg,only", [("tiny", p) for p in ("plan", "stitch", "fix_ends_plan", "slice", "ou_prep",
-                                                              "ou_scan", "ou_compact")]
-                         + [("tiny", ""), ("rtiny", "")])
-def test_draft_device_multi_launch_passes(cfg, only, monkeypatch):
-    """Every table pass (or one, `only`) in the count / scan / fill form."""
+@pytest.mark.parametrize("cfg,only,scan", [("tiny", p, "0") for p in ("plan", "stitch", "fix_ends_plan", "slice",
+                                                                       "ou_prep", "ou_scan", "ou_compact")]
+                         + [("tiny", "", "0"), ("rtiny", "", "0"), ("tiny", "", "1"), ("rtiny", "", "1")])
+def test_draft_device_multi_launch_passes(cfg, only, scan, monkeypatch):
+    """Every table pass (or one, `only`) in its many-workgroup form: one
+    launch with decoupled look-back over 256-block tiles, or (scan=1) count /
+    rocPRIM scan / fill launches."""
     monkeypatch.setenv("NPGX_ELF_PASS_WG", "0")
     monkeypatch.setenv("NPGX_ELF_PASS_MULTI", only)
+    monkeypatch.setenv("NPGX_ELF_PASS_SCAN", scan)
     b_dev, d_dev, s_dev = _draft(cfg, True, monkeypatch)
     b_host, d_host, s_host = _draft(cfg, False, monkeypatch)
     assert canon(b_dev) == canon(b_host)

@@ -365,6 +365,9 @@ def run_pairs(args, dist, world, rank, local_rank, comm, config, n_pairs, steps,
                     "note": "HIP-event kernel times of every pair of the rank, each pair's collected on its "
                             "worker right after it ran; concurrent pairs' events overlap, so this understates "
                             "the kernel's rate"}
+        # HBM traffic per launch from the pair workload's own PMC passes
+        # (profiles/*_<config>pairs_pmc_traffic.json, tools/round_end.sh)
+        roofline.update(pmc_traffic(dom["name"], config + "pairs"))
     cpu = None
     if rank == 0 and world == 1 and baseline:
         cpu = cpu_baseline_pair(names, seqs, sel, cpu_runs or args.cpu_runs)
@@ -467,6 +470,12 @@ def pmc_traffic(kernel, config):
     doc = json.load(open(files[-1]))
     for name, v in doc["kernels"].items():
         if name.split("::")[-1].split("<")[0] == "k_" + kernel:  # (k_align_jobs<true>: the kernel's forms)
+            if "active_traffic_bytes_per_launch" in v:  # launches that read something (the timed ones)
+                return {"traffic": v["active_traffic_bytes_per_launch"], "traffic_source": os.path.basename(files[-1]),
+                        "traffic_fetch": v["active_fetch_bytes_per_launch"],
+                        "traffic_write": v["active_write_bytes_per_launch"],
+                        "traffic_launches": "active (%d of %d dispatches read memory)" % (v["active_dispatches"],
+                                                                                          v["dispatches"])}
             return {"traffic": v["traffic_bytes_per_launch"], "traffic_source": os.path.basename(files[-1]),
                     "traffic_fetch": v["fetch_bytes_per_launch"], "traffic_write": v["write_bytes_per_launch"]}
     return {"traffic": None}

@@ -40,6 +40,10 @@ else
   step rocprof_c3
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/prof_c3.log 2>&1 || { tail -5 $O/prof_c3.log; exit 1; }
+  python3 $R/tools/step_timeline.py $O/prof_c3/run_kernel_trace.csv > $O/c3_step_timeline.txt 2>&1 || true
+  step rocprof_c2
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2 -o run -- python3 $R/bench.py --config C2 --steps 3 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/prof_c2.log 2>&1 || { tail -5 $O/prof_c2.log; exit 1; }
+  python3 $R/tools/step_timeline.py $O/prof_c2/run_kernel_trace.csv > $O/c2_step_timeline.txt 2>&1 || true
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_$c
     timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/c3_$c -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/pmc_$c.log 2>&1 || { tail -5 $O/pmc_$c.log; exit 1; }

@@ -3078,7 +3078,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // budget shrinks as more workgroups must be resident per CU.
         int64_t max_rows = 0;
         for (int32_t j : todo) max_rows = std::max<int64_t>(max_rows, jsum[j]);
-        const int64_t per_cu = std::min<int64_t>(4 * SA_WAVES_PER_EU, std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
+        static const int64_t per_cu_max = getenv("NPGX_SA_PER_CU_MAX") ? std::max(1, atoi(getenv("NPGX_SA_PER_CU_MAX")))
+                                                                       : 4 * SA_WAVES_PER_EU;  // (A/B: LDS per slot)
+        const int64_t per_cu = std::min<int64_t>(std::min<int64_t>(4 * SA_WAVES_PER_EU, per_cu_max),
+                                                 std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
         const int64_t budget = LDS_PER_CU / per_cu;
         // word history of the row-parallel search (HIST_SHIFTS x 64 words) when
         // the budget allows
@@ -3481,6 +3484,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             res.cap.clear();
             res.bptr.clear();
             al->host_ms[0] += ms(tp);
+            pmark(8);
+            if (pdbg)
+                fprintf(stderr, "align_device async %d jobs: prep %.3f order %.3f puts %.3f split_plan %.3f slots %.3f "
+                        "args %.3f lds+split %.3f launch %.3f post %.3f ms\n", n_jobs, pt[0], pt[1], pt[2], pt[3],
+                        pt[4], pt[5], pt[6], pt[7], pt[8]);
             return;
         }
         int32_t* pl = (int32_t*)al->pinned.take((size_t)n_jobs * 8 + 8, st);

@@ -2649,7 +2649,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     }
     static const bool pdbg = getenv("NPGX_PREP_DEBUG") != nullptr;  // host phase times to stderr
     double pt[12] = {0};
-    auto pt0 = std::chrono::steady_clock::now();
+    auto pt0 = tp;  // (phase 0: the per-job loop above)
     auto pmark = [&](int i) {
         if (!pdbg) return;
         pt[i] += ms(pt0);

@@ -125,7 +125,8 @@ struct SaArgs {
     SaSub* subs;
     int2* sub_res;             // per sub-job: columns (-1: overflow), identical columns after
     unsigned long long* alloc; // [0] pool bytes taken, [1] sub-jobs issued
-    unsigned int* counters;    // [0] next sub-job, [1] deferred jobs, [2] next deferred job
+    unsigned int* counters;    // [0] next sub-job, [1] deferred jobs, [2] next deferred job,
+                               // [3] sub-jobs re-run in place, [4] next retried sub-job, [5] retried sub-jobs
     unsigned char* pool;       // per sub-job: 64 row lengths (int32), then n rows x out_cap
     int64_t pool_cap;
     int64_t max_sub;
@@ -143,6 +144,7 @@ struct SaArgs {
     unsigned int* sctr;
     int32_t* qseg;
     int32_t* qsub;
+    const int32_t* rq;         // k_align_sub's retry launch: the failed sub-jobs (count in counters[5])
     int2* ftasks;
     unsigned char* post_area;  // k_split_post's global work areas (SaSplit.post)
     int4* chain;               // per job split, from its seg0: the chain (segment, columns, first column)
@@ -900,12 +902,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
     SlotEnv e = slot_env(a, lds_u64);
     uint32_t epoch = next_epoch(a), lepoch = 0;
     const unsigned int n_sub = (unsigned int)a.alloc[1];
-    const bool planned = a.sctr != nullptr;
+    // retry launch (a.rq): the sub-jobs whose split chain failed or that
+    // overflowed, each whole in a room of its rows' total length
+    const bool retry = a.rq != nullptr;
+    const bool planned = !retry && a.sctr != nullptr;
     const unsigned int nseg = planned ? a.sctr[SC_QSEG] : 0u;
-    const unsigned int nq = planned ? nseg + a.sctr[SC_QSUB] : n_sub;
+    const unsigned int nq = retry ? a.counters[5] : planned ? nseg + a.sctr[SC_QSUB] : n_sub;
     while (true) {
         unsigned int qn = 0;
-        if (lane == 0) qn = atomicAdd(&a.counters[0], 1u);
+        if (lane == 0) qn = atomicAdd(&a.counters[retry ? 4 : 0], 1u);
         qn = bcast(qn, 0);
         if (qn >= nq) break;
         const bool seg = qn < nseg;
@@ -918,7 +923,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
             sp = a.splits[sg.split];
             sn = sp.sub;
         } else {
-            sn = planned ? a.qsub[qn - nseg] : (int)qn;
+            sn = retry ? a.rq[qn] : planned ? a.qsub[qn - nseg] : (int)qn;
         }
         const SaSub d = a.subs[sn];
         const SaJob job = a.jobs[d.job];
@@ -939,8 +944,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         }
         char* out = seg ? (char*)(a.seg_pool + sg.out) : (char*)(a.pool + d.out_off + 256);
         int ocap = d.out_cap;  // (a re-run below moves the output)
+        if (retry) {  // a new room at the proven bound, from the pool
+            const int tot = wave_sum(w.act ? v.len : 0);
+            const int room = min(cap, (tot + 15) & ~15);
+            long long off2 = -1;
+            if (lane == 0) off2 = reserve(&a.alloc[0], (unsigned long long)sub_bytes(n, room),
+                                          (unsigned long long)a.pool_cap);
+            off2 = (long long)bcast64((unsigned long long)off2, 0);
+            if (off2 < 0) {  // pool full: the job re-runs whole, as before
+                if (lane == 0) a.sub_res[sn] = make_int2(-1, 0);
+                __syncthreads();
+                continue;
+            }
+            if (w.act) ((int*)(a.pool + off2))[lane] = ((const int*)(a.pool + d.out_off))[lane];
+            if (lane == 0) {
+                SaSub d2 = d;
+                d2.out_off = off2;
+                d2.out_cap = room;
+                a.subs[sn] = d2;
+            }
+            out = (char*)(a.pool + off2 + 256);
+            ocap = room;
+        }
         const unsigned long long w_start = wall_clock64();
-        ProcT<LONG> pr(w, a.P, e.S, out, seg ? sg.cap : d.out_cap, epoch, lepoch);
+        ProcT<LONG> pr(w, a.P, e.S, out, seg ? sg.cap : ocap, epoch, lepoch);
         int Lc = 0;
         bool ovf = false;
         if (!idle) {
@@ -1002,6 +1029,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         __syncthreads();
     }
     if (lane == 0) atomicMax(a.slot_epoch, epoch);
+}
+
+// the sub-jobs to retry: failed (columns -1) after their segments' chain or
+// their own run, whole ones only (a twin's stays with its job)
+__global__ void k_sub_retry_list(SaArgs a) {
+    const unsigned int n_sub = (unsigned int)a.alloc[1];
+    for (unsigned int sn = blockIdx.x * blockDim.x + threadIdx.x; sn < n_sub; sn += gridDim.x * blockDim.x)
+        if (a.sub_res[sn].x < 0 && a.subs[sn].pad >= 0)
+            ((int32_t*)a.rq)[atomicAdd(&a.counters[5], 1u)] = (int32_t)sn;
 }
 
 // k_align_finish: realing_end on the deferred jobs' B (= good regions of A +
@@ -2537,6 +2573,7 @@ struct npgx_aligner {
     DevBuf<unsigned int> d_sctr;
     DevBuf<unsigned char> d_seg_pool;
     DevBuf<int> d_reg_dst;  // k_fin_copy's region offsets when they do not fit its LDS
+    DevBuf<int32_t> d_rq;   // k_align_sub's retry launch: failed sub-jobs
     // last result
     std::vector<char> out;
     std::vector<int64_t> out_off;
@@ -3040,11 +3077,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             al->d_subs.grow((size_t)max_sub);
             al->d_sub_res.grow((size_t)max_sub);
             al->d_alloc.ensure(2);
-            al->d_counters.ensure(4);
+            al->d_counters.ensure(8);
             // sub-job outputs: about what the jobs' own scratch holds
             al->d_pool.grow((size_t)scratch + (16u << 20));
             zero(al->d_alloc.p, 16);
-            zero(al->d_counters.p, 16);
+            zero(al->d_counters.p, 32);
             A.job_regions = al->d_job_regions.p;
             A.job_nreg = al->d_job_nreg.p;
             A.subs = al->d_subs.p;
@@ -3117,6 +3154,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.sctr = nullptr;
         A.qseg = nullptr;
         A.qsub = nullptr;
+        A.rq = nullptr;
         A.ftasks = nullptr;
         A.split_len = o.aligner_type == 0 ? al->split : 0;
         A.twin_rows = nullptr;
@@ -3288,6 +3326,19 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             if (split_subs) {  // the split sub-jobs' chains
                 ti = al->timer.begin("align_sub_post", st, 0.0, 0);
                 hipLaunchKernelGGL(k_sub_post, dim3(512), dim3(POST_THREADS), 0, st, A, n_job_splits, -1);
+                NPGX_HIP(hipGetLastError());
+                al->timer.end(ti, st);
+                // the failed sub-jobs again, whole, at their proven bound (one
+                // launch, usually empty): a split sub-job whose chain broke or
+                // overflowed no longer sends its job to attempt 1 whole
+                // 
+                al->d_rq.grow((size_t)std::max<int64_t>(n_sub_max, 1));
+                SaArgs A2 = A;
+                A2.rq = al->d_rq.p;
+                ti = al->timer.begin("align_sub_retry", st, 0.0, 0);
+                hipLaunchKernelGGL(k_sub_retry_list, dim3(256), dim3(256), 0, st, A2);
+                if (al->long_head > 0) hipLaunchKernelGGL(k_align_sub<true>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A2);
+                else hipLaunchKernelGGL(k_align_sub<false>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A2);
                 NPGX_HIP(hipGetLastError());
                 al->timer.end(ti, st);
             }

@@ -907,7 +907,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
     const bool retry = a.rq != nullptr;
     const bool planned = !retry && a.sctr != nullptr;
     const unsigned int nseg = planned ? a.sctr[SC_QSEG] : 0u;
-    const unsigned int nq = retry ? a.counters[5] : planned ? nseg + a.sctr[SC_QSUB] : n_sub;
+    const unsigned int nq = retry ? (unsigned int)min((int64_t)a.counters[5], a.max_sub)
+                                  : planned ? nseg + a.sctr[SC_QSUB] : n_sub;
     while (true) {
         unsigned int qn = 0;
         if (lane == 0) qn = atomicAdd(&a.counters[retry ? 4 : 0], 1u);
@@ -1036,8 +1037,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
 __global__ void k_sub_retry_list(SaArgs a) {
     const unsigned int n_sub = (unsigned int)a.alloc[1];
     for (unsigned int sn = blockIdx.x * blockDim.x + threadIdx.x; sn < n_sub; sn += gridDim.x * blockDim.x)
-        if (a.sub_res[sn].x < 0 && a.subs[sn].pad >= 0)
-            ((int32_t*)a.rq)[atomicAdd(&a.counters[5], 1u)] = (int32_t)sn;
+        if (a.sub_res[sn].x < 0 && a.subs[sn].pad >= 0) {
+            const unsigned int q = atomicAdd(&a.counters[5], 1u);  // (< n_sub <= max_sub, rq's size)
+            if ((int64_t)q < a.max_sub) ((int32_t*)a.rq)[q] = (int32_t)sn;
+        }
 }
 
 // k_align_finish: realing_end on the deferred jobs' B (= good regions of A +

@@ -2537,10 +2537,11 @@ struct npgx_aligner {
     int long_head = 128;
     int long_m = 512;
     // split jobs whose segment rooms for the whole row suffixes take at most
-    // this many bytes get them (NPGX_SEG_FULL_MB; default 0: the 8-sync-state
-    // rooms -- 64 MB took R3's re-run jobs from 7 to 4 and no time off:
-    // their overflows are sub-jobs', gpurun_out/r05m)
-    int64_t seg_full_bytes = 0;
+    // this many bytes get them (NPGX_SEG_FULL_MB; 0: the 8-sync-state rooms).
+    // R3: the segment overflows (reason 202) go with them; the sub-job
+    // overflows that were left (reason 10, gpurun_out/r05m) re-run in the
+    // sub-job retry launch
+    int64_t seg_full_bytes = 64ll << 20;
     // twins of the split jobs (NPGX_TWINS: 0 never -- the default: measured at
     // C3 and C5 the whole-job bad region they serve is rare among split jobs
     // and their segments slow the launch -- 1 always, -1 in launches with few

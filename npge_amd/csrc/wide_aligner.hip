@@ -70,6 +70,7 @@ struct WArgs {
     int32_t* len_out;
     int32_t* status;          // 0 ok, 1 re-run larger, 2 refused
     int mc, gc, ac, min_length, wf, aligner_type;
+    int lh, lm;               // try_aligned: incremental shifts before the prefix search (0: never), its first prefix
 };
 
 struct Frame {
@@ -338,6 +339,7 @@ struct Job {
         for (uint32_t q = threadIdx.x; q < nw; q += WT) {
             wk[wu[q]] = EMPTY;
             wc[wu[q]] = 0;
+            pt[wu[q]] = EMPTY;  // (the prefix search keeps a word's state at its key's slot)
         }
         __threadfence();
         __syncthreads();
@@ -377,6 +379,119 @@ struct Job {
             h = (h + 1) & mask;
         }
     }
+    // try_aligned past the first lh shifts (the batched aligner's
+    // find_word_long, sa_device.hpp, for a workgroup): for a prefix [0, M)
+    // of shifts, T(w) = the shift at which the last row first sights word w
+    // and S* = min T(w) is where the shift-by-shift loop stops.  A complete
+    // word is one of row 0's words, so the word table holds row 0's words of
+    // the prefix, each with a state at its key's slot in pt packed as
+    // (~rows that have sighted it) << 32 | T, lowered by atomicMin (more rows,
+    // then the earlier sighting, win).  Rows 1..n-1 pass over the prefix in
+    // order, 4 x WT shifts a step, every state read before any of the step's
+    // atomics: row k raises only words all of rows 0..k-1 have sighted, at
+    // its first sighting.  No complete word: the prefix doubles (from lm) up
+    // to max_shift.  At S* the loop's own tests follow (one word in every
+    // row; else the word of the highest row complete at S*) and every row's
+    // first sighting of it.
+    __device__ static unsigned long long pstate(uint32_t rows, uint32_t t) {
+        return ((unsigned long long)(0xFFFFFFFFu - rows) << 32) | t;
+    }
+    __device__ bool prefix_search(Frame& F, int max_shift) {
+        const int ac = a.ac;
+        bool found = false;
+        for (int M = min(max(a.lm, a.lh + 1), max_shift);; M = min(2 * M, max_shift)) {
+            if ((uint32_t)M > tcap / 2) {  // row 0's words would not fit: a larger table (status 1)
+                fail(1);
+                break;
+            }
+            __syncthreads();
+            {
+                const RowV v0 = F.rv[0];
+                for (int s = threadIdx.x; s < M; s += WT) {
+                    const uint32_t h = word_slot(word_at(v0, F.dir, v0.pos + s, ac), true);
+                    atomicMin(pt + h, pstate(1, (uint32_t)s));
+                }
+            }
+            __threadfence();
+            __syncthreads();
+            for (int k = 1; k < n; k++) {
+                const RowV v = F.rv[k];
+                for (int s0 = 0; s0 < M; s0 += 4 * WT) {
+                    uint32_t hs[4];
+                    unsigned long long nv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int s = s0 + u * WT + (int)threadIdx.x;
+                        hs[u] = ~0u;
+                        if (s < M) {
+                            const uint32_t h = word_slot(word_at(v, F.dir, v.pos + s, ac), false);
+                            if (h != ~0u) {
+                                const unsigned long long st = aload(pt + h);
+                                if (0xFFFFFFFFu - (uint32_t)(st >> 32) == (uint32_t)k) {
+                                    hs[u] = h;
+                                    nv[u] = pstate((uint32_t)k + 1, max((uint32_t)st, (uint32_t)s));
+                                }
+                            }
+                        }
+                    }
+                    __syncthreads();  // every state of the step read before its atomics
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (hs[u] != ~0u) atomicMin(pt + hs[u], nv[u]);
+                    __threadfence();
+                    __syncthreads();
+                }
+            }
+            // S*: the smallest T of a word all n rows have sighted
+            int tmin = 0x7fffffff;
+            {
+                const RowV v0 = F.rv[0];
+                for (int s = threadIdx.x; s < M; s += WT) {
+                    const uint32_t h = word_slot(word_at(v0, F.dir, v0.pos + s, ac), false);
+                    const unsigned long long st = h != ~0u ? aload(pt + h) : EMPTY;
+                    if (0xFFFFFFFFu - (uint32_t)(st >> 32) == (uint32_t)n) tmin = min(tmin, (int)(uint32_t)st);
+                }
+            }
+            const int S = lds_min(*C, tmin);
+            if (S < M) {
+                const RowV v0 = F.rv[0];
+                const unsigned long long w0 = word_at(v0, F.dir, v0.pos + S, ac);
+                bool same = true;
+                int cand = -1;
+                for (int i = threadIdx.x; i < n; i += WT) {
+                    const RowV v = F.rv[i];
+                    const unsigned long long w = word_at(v, F.dir, v.pos + S, ac);
+                    same &= w == w0;
+                    const uint32_t h = word_slot(w, false);
+                    const unsigned long long st = h != ~0u ? aload(pt + h) : EMPTY;
+                    if (0xFFFFFFFFu - (uint32_t)(st >> 32) == (uint32_t)n && (int)(uint32_t)st <= S) cand = i;
+                }
+                if (__syncthreads_and(same)) {
+                    for (int i = threadIdx.x; i < n; i += WT) F.rv[i].pad = S;
+                } else {
+                    cand = lds_max(*C, cand);  // (>= 0: the row that sighted S*'s word last holds it at S*)
+                    if (threadIdx.x == (unsigned)(cand % WT)) {
+                        const RowV v = F.rv[cand];
+                        C->best = word_at(v, F.dir, v.pos + S, ac);
+                    }
+                    __syncthreads();
+                    const unsigned long long best = C->best;
+                    for (int i = threadIdx.x; i < n; i += WT) {
+                        const RowV v = F.rv[i];
+                        int s = 0;
+                        while (s < S && word_at(v, F.dir, v.pos + s, ac) != best) s++;
+                        F.rv[i].pad = s;
+                    }
+                }
+                found = true;
+            }
+            clear_tables();
+            if (found || failed() || M >= max_shift) break;
+        }
+        __syncthreads();
+        return found;
+    }
+
     __device__ bool try_aligned(Frame& F, int tail, int& d, int col) {
         if (failed()) return false;
         const int ac = a.ac;
@@ -384,7 +499,11 @@ struct Job {
         if (max_shift <= 0) return false;
         bool found = false;
         int shift = 0;
-        for (; shift < max_shift; shift++) {
+        // the first lh shifts incrementally (most searches end there), then
+        // whole prefixes (prefix_search)
+        const bool lng = a.lh > 0 && max_shift > a.lh;
+        const int head = lng ? a.lh : max_shift;
+        for (; shift < head; shift++) {
             __syncthreads();
             if (C->n_pu + (uint32_t)n > tcap / 2 || C->n_wu + (uint32_t)n > tcap / 2) {
                 fail(1);
@@ -431,6 +550,7 @@ struct Job {
             }
         }
         clear_tables();
+        if (!found && lng && !failed()) found = prefix_search(F, max_shift);
         if (!found || failed()) return false;
         // append_aligned: the reversed prefixes [pos, pos + shift_i) as a child frame
         long long sum = 0;
@@ -1011,6 +1131,12 @@ void align_wide(WideBufs* W, hipStream_t st, const char* d_rows, const int64_t* 
             A.min_length = params[3];
             A.wf = params[4];
             A.aligner_type = aligner_type;
+            // try_aligned's prefix search after the first WIDE_LONG_HEAD shifts
+            // (NPGX_WIDE_LONG_HEAD; 0: shift by shift only, the round-4 search)
+            const char* wl = getenv("NPGX_WIDE_LONG_HEAD");  // (read per batch: tests switch it)
+            const int wlh = wl && *wl ? std::max(0, atoi(wl)) : 128;
+            A.lh = wlh;
+            A.lm = 512;
             hipLaunchKernelGGL(k_align_wide, dim3((unsigned)nw), dim3(WT), 0, st, A);
             NPGX_HIP(hipGetLastError());
             std::vector<int32_t> L(nw), S(nw);

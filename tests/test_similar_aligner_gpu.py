@@ -310,6 +310,23 @@ def test_refine_random(seed):
             assert g == orc.align(a, mode="refine"), a
 
 
+@pytest.mark.parametrize("head", ["128", "1", "0"])
+def test_wide_long_restart_searches(head, monkeypatch):
+    """The wide aligner's prefix search (prefix_search, wide_aligner.hip)
+    against the oracle: more than 64 rows with unrelated insertions of up to
+    3000 bases between shared stretches, repeats planted in the insertions,
+    unrelated tails.  NPGX_WIDE_LONG_HEAD moves the switch from the shift-by-
+    shift search (0: never switch)."""
+    monkeypatch.setenv("NPGX_WIDE_LONG_HEAD", head)
+    rng = np.random.default_rng(77)
+    jobs = []
+    for n in (65, 90, 130):
+        for ins, rep in ((300, 0.0), (1500, 0.5), (3000, 0.0)):
+            jobs.append(_restart_family(rng, n, 200, ins, repeat=rep))
+    jobs.append(_family(rng, 80, 400, 0.02, tail_unrelated=0.5))
+    _check(jobs)
+
+
 def test_wide_unrelated_long_tails():
     """More than 64 rows whose homology ends after a short core, followed by
     unrelated tails of 20k+ bases: the wide aligner's word

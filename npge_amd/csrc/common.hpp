@@ -206,7 +206,9 @@ struct StageTimer {
         for (const Rec& r : recs) {
             if (k >= cap) break;
             float ms = 0.f;
-            if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = -1.f;
+            // (the end marker may still be in the queue when the caller waited on
+            // the work itself, not on the marker: wait for it)
+            if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) ms = -1.f;
             snprintf(out[k].name, sizeof(out[k].name), "%s", r.name.c_str());
             out[k].ms = ms;
             out[k].bytes = r.bytes;

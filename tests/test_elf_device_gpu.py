@@ -179,3 +179,25 @@ def test_extend_loop_fast_device_host_fallback(monkeypatch):
     o.apply("DummyAligner")
     o.apply("ExtendLoopFast")
     assert canon(o.blocks()) == res[0][0]
+
+
+def test_blockset_tune(monkeypatch):
+    """npgx_blockset_tune: "long-head" (the aligner forms without the prefix
+    search's call at 0) and "elf-device" change no result; unknown keys and
+    values out of range are refused."""
+    from npge_amd import _capi
+    from npge_amd.anchor_finder import AnchorFinder
+    monkeypatch.delenv("NPGX_ELF_DEVICE", raising=False)
+    names, seqs = synth.genome_set("rtiny")
+    res = []
+    for tune in ({}, {"long-head": 0}, {"elf-device": 0}, {"long-head": 0, "elf-device": 1}):
+        ss, eng = _engine(seqs, names)
+        for k, v in tune.items():
+            eng.tune(k, v)
+        eng.apply("DraftPangenome", af=AnchorFinder())
+        res.append((canon(eng.blocks()), eng.rows_digest()))
+    assert all(r == res[0] for r in res[1:])
+    ss, eng = _engine(seqs, names)
+    for k, v in (("no-such-key", 1), ("elf-device", 2), ("long-head", -1)):
+        with pytest.raises(_capi.NpgxError):
+            eng.tune(k, v)

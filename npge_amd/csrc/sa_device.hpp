@@ -75,10 +75,6 @@ static constexpr int VEC_ROWS = 8;
 #define SA_FAST_ROWS 1
 #endif
 static constexpr int FR = SA_FAST_ROWS;  // fast_run: rows loaded per batch
-#ifndef SA_FW_GROUPS  // (A/B builds: 1 = find_word's one group of J shifts a step)
-#define SA_FW_GROUPS 4
-#endif
-static constexpr int FW_G = SA_FW_GROUPS;  // try_aligned's row-parallel search: groups of J shifts a step
 typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // LDS-qualified word-table entry
 typedef __attribute__((address_space(3))) uint32_t LdsU32;
 static constexpr int HIST_SHIFTS = 32;  // words per lane kept for the first-sighting scan  // try_aligned with lanes = shifts up to this many rows
@@ -1062,23 +1058,12 @@ struct ProcT {
             if (r.found < 0) table_full();
             if (r.found != 0 || !lng) return r.found > 0;
         } else {
-            // G = 4 groups of J shifts a step where the table holds them (find_word_g)
-            // (the forms without the prefix search keep find_word: less scratch for the pair workers)
-            const int r = LONG && S.ltab_log2 >= 10
-                              ? find_word_g<LdsU64, LdsU32, FW_G>(my_shift, head, (LdsU64*)S.lkeys, (LdsU64*)S.lmask,
-                                                                  (LdsU32*)S.ldone, S.ltab_log2, lepoch,
-                                                                  1 << (S.ltab_log2 - 1))
-                              : find_word<LdsU64, LdsU32>(my_shift, head, (LdsU64*)S.lkeys, (LdsU64*)S.lmask,
-                                                          (LdsU32*)S.ldone, S.ltab_log2, lepoch, 1 << (S.ltab_log2 - 1));
+            const int r = find_word<LdsU64, LdsU32>(my_shift, head, (LdsU64*)S.lkeys, (LdsU64*)S.lmask,
+                                                    (LdsU32*)S.ldone, S.ltab_log2, lepoch, 1 << (S.ltab_log2 - 1));
             if (r == 1 || (r == 0 && !lng)) return r == 1;
             if (r < 0) {
-                const int g = LONG && S.tcap_log2 >= 11
-                                  ? find_word_g<unsigned long long, uint32_t, FW_G>(
-                                        my_shift, head, S.tkeys, S.tmask, S.tdone, S.tcap_log2, epoch,
-                                        (1 << (S.tcap_log2 - 1)) - 64 * FW_G)
-                                  : find_word<unsigned long long, uint32_t>(my_shift, head, S.tkeys, S.tmask, S.tdone,
-                                                                            S.tcap_log2, epoch,
-                                                                            (1 << (S.tcap_log2 - 1)) - 64);
+                const int g = find_word<unsigned long long, uint32_t>(my_shift, head, S.tkeys, S.tmask, S.tdone,
+                                                                      S.tcap_log2, epoch, (1 << (S.tcap_log2 - 1)) - 64);
                 if (g < 0) table_full();
                 if (g != 0 || !lng) return g == 1;
             }
@@ -1102,212 +1087,6 @@ struct ProcT {
     __device__ __forceinline__ void table_full() {
         ovf = true;
         stop = true;
-    }
-
-    // find_word with G groups of J shifts per step (more than VEC_ROWS rows,
-    // so J = 64/n <= 7; the table holds at least 256 G entries): group g's
-    // lane (j, r) holds row r's word at shift s0 + g J + j.  Every word of the
-    // step claims its key, the row's first sighting within the step is its
-    // lowest shift with the word over all the step's groups (shuffle
-    // compares), then one round of row-mask / done atomics and one of
-    // completeness tests serves G J shifts: the step's latency (two barriers,
-    // three dependent table accesses) is paid once per G J shifts instead of
-    // once per J.  The first complete shift is the lowest group's lowest j;
-    // what follows is find_word's.
-    template <class T, class U, int G>
-    __device__ __forceinline__ int find_word_g(int& my_shift, int max_shift, T* tkeys, T* tmask, U* tdone,
-                                               uint32_t tlog, uint32_t& ep_ref, int limit) {
-        uint32_t ep32 = ep_ref + 1;
-        const uint32_t tcap = 1u << tlog;
-        if (ep32 >= 0xFFFF) {  // epoch wrap: clear the table
-            for (uint32_t i = w.lane; i < tcap; i += 64) {
-                tkeys[i] = 0ull;
-                tmask[i] = 0ull;
-            }
-            __threadfence();
-            ep32 = 1;
-        }
-        ep_ref = ep32;
-        const unsigned long long ep = (unsigned long long)ep32 << 48;
-        const int ac = P.ac;
-        const unsigned long long wmask = (ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * ac)) - 1);
-        const int n = w.n;
-        const int J = 64 / n;  // (n > VEC_ROWS: J <= 7)
-        const int SJ = G * J;  // shifts per step
-        const int r = w.lane % n, j = w.lane / n;
-        const bool act = j < J;
-        const View vr{shfl_ptr(v.p, r), __shfl(v.len, r), __shfl(v.d, r)};
-        const int pr = __shfl(pos, r);
-        LdsU64* hw = (LdsU64*)S.lwords;
-        const int hist = S.hist_cap > 0 ? S.hist_cap * 64 / n : 0;
-        unsigned long long word = 0;  // the lane's word of the previous group
-        int nxt = pr + j + ac - 1;    // next char of this lane's word
-        if (act) {
-            int c[15];
-#pragma unroll
-            for (int t = 0; t < 15; t++) c[t] = t < ac - 1 ? vch(vr, pr + j + t, r) : 0;  // independent loads
-#pragma unroll
-            for (int t = 0; t < 15; t++)
-                if (t < ac - 1) word = (word << 3) | code3(c[t]);
-        }
-        int inserted = 0;
-        for (int s0 = 0; s0 < max_shift; s0 += SJ) {
-            // the step's chars: group 0 adds 1 (first step) or J, every further group J
-            const int add0 = s0 == 0 ? 1 : J;
-            const int tot = add0 + (G - 1) * J;
-            int ch[G * 7];
-#pragma unroll
-            for (int t = 0; t < G * 7; t++) ch[t] = (act && t < tot) ? vch(vr, nxt + t, r) : 0;
-            nxt += tot;
-            unsigned long long wg[G];
-#pragma unroll
-            for (int g = 0; g < G; g++) wg[g] = 0;
-#pragma unroll
-            for (int t = 0; t < G * 7; t++) {
-                if (t < tot) word = ((word << 3) | code3(ch[t])) & wmask;
-#pragma unroll
-                for (int g = 0; g < G; g++)
-                    if (t + 1 == add0 + g * J) wg[g] = word;  // group g's word: after its last char
-            }
-            int sg[G];
-            bool valid[G];
-            uint32_t slot[G];
-            bool claimed[G];
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                sg[g] = s0 + g * J + j;
-                valid[g] = act && sg[g] < max_shift;
-                if (valid[g] && sg[g] < hist) hw[sg[g] * n + r] = wg[g];
-                const unsigned long long key = ep | wg[g];
-                slot[g] = 0;
-                claimed[g] = false;
-                if (valid[g]) {
-                    uint32_t sl = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tlog));
-                    while (true) {
-                        unsigned long long k = __hip_atomic_load(&tkeys[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (k == key) break;
-                        if ((k & ~((1ull << 48) - 1)) != ep) {  // stale or empty: claim
-                            if (__hip_atomic_compare_exchange_strong(&tkeys[sl], &k, key, __ATOMIC_RELAXED,
-                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                                claimed[g] = true;
-                                break;
-                            }
-                            if (k == key) break;  // another lane claimed the same word
-                            continue;
-                        }
-                        sl = (sl + 1) & (tcap - 1);
-                    }
-                    slot[g] = sl;
-                }
-                if (claimed[g]) {
-                    __hip_atomic_store(&tmask[slot[g]], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&tdone[slot[g]], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            // the row's lowest shift with the word in this step: lower j of the
-            // same group, any j of an earlier group
-            bool first[G];
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                first[g] = valid[g];
-                for (int jj = 1; jj < J; jj++) {
-                    const unsigned long long o = shfl64(wg[g], max(w.lane - jj * n, 0));
-                    if (jj <= j && o == wg[g]) first[g] = false;
-                }
-#pragma unroll
-                for (int g2 = 0; g2 < G; g2++) {
-                    if (g2 >= g) break;
-                    for (int j2 = 0; j2 < J; j2++) {
-                        const unsigned long long o = shfl64(wg[g2], j2 * n + r);
-                        if (o == wg[g]) first[g] = false;
-                    }
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int g = 0; g < G; g++)
-                if (first[g]) {
-                    const unsigned long long old = __hip_atomic_fetch_or(&tmask[slot[g]], 1ull << r, __ATOMIC_RELAXED,
-                                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    if (!((old >> r) & 1ull))
-                        __hip_atomic_fetch_max(&tdone[slot[g]], (uint32_t)sg[g], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                }
-            __syncthreads();
-            unsigned long long cm[G];
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                bool complete = false;
-                if (valid[g])
-                    complete =
-                        __hip_atomic_load(&tmask[slot[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == w.rowmask &&
-                        (int)__hip_atomic_load(&tdone[slot[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= sg[g];
-                inserted += __popcll(ballot(claimed[g]));
-                cm[g] = ballot(complete);
-            }
-            n_shifts += min(SJ, max_shift - s0);
-            int gm = -1;
-            unsigned long long cmf = 0, wsel = 0;
-#pragma unroll
-            for (int g = G - 1; g >= 0; g--)
-                if (cm[g]) {
-                    gm = g;
-                    cmf = cm[g];
-                    wsel = wg[g];
-                }
-            if (gm >= 0) {
-                // the first complete shift (lowest group, lowest j), its highest complete row names the word
-                const int jm = (__ffsll((long long)cmf) - 1) / n;
-                const unsigned long long rows = (cmf >> (jm * n)) & w.rowmask;
-                const int rb = 63 - __clzll((long long)rows);
-                const unsigned long long best = bcast64(wsel, jm * n + rb);
-                const int sb = s0 + gm * J + jm;
-                const unsigned long long same = ballot(act && j == jm && wsel == bcast64(wsel, jm * n));
-                if (((same >> (jm * n)) & w.rowmask) == w.rowmask) {  // words.size() == 1
-                    my_shift = sb;
-                } else {
-                    my_shift = -1;
-                    if (sb < hist) {
-                        if (w.act)
-                            for (int t = 0; t <= sb; t++)
-                                if (hw[t * n + w.lane] == best) {
-                                    my_shift = t;
-                                    break;
-                                }
-                    } else {
-                        // rescan the rows J shifts per step in find_word's lane layout
-                        unsigned long long x = 0;
-                        if (act)
-                            for (int q = 0; q < ac - 1; q++) x = (x << 3) | code3(vch(vr, pr + j + q, r));
-                        int at = pr + j + ac - 1, fs = -1;
-                        unsigned long long found = 0;  // rows with a first sighting
-                        for (int t0 = 0; t0 <= sb && (found & w.rowmask) != w.rowmask; t0 += J) {
-                            const int add = t0 == 0 ? 1 : J;
-                            if (act)
-                                for (int t = 0; t < add; t++) x = ((x << 3) | code3(vch(vr, at + t, r))) & wmask;
-                            at += add;
-                            const bool hit = act && t0 + j <= sb && x == best;
-                            const unsigned long long hm = ballot(hit);
-                            if (hit && fs < 0 && !((found >> r) & 1ull)) {
-                                bool lowest = true;
-                                for (int jj = 1; jj <= j; jj++) lowest &= !((hm >> (w.lane - jj * n)) & 1ull);
-                                if (lowest) fs = t0 + j;
-                            }
-                            for (int q = 0; q < J; q++) found |= (hm >> (q * n)) & w.rowmask;
-                        }
-                        int got = -1;
-                        for (int q = 0; q < J; q++) {
-                            const int o = __shfl(fs, q * n + (w.lane < n ? w.lane : 0));
-                            if (got < 0 && o >= 0) got = o;
-                        }
-                        if (w.act) my_shift = got;
-                    }
-                }
-                return 1;
-            }
-            if (inserted > limit) return -1;
-        }
-        return 0;
     }
 
     // 1: found (my_shift set), 0: no shift works, -1: more than `limit` inserts

@@ -2810,7 +2810,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         const int64_t per1 = (20ll << tlog1) + 1028ll * depth1 + 17ll * cols1;
         slots1 = (size_t)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>((int64_t)order.size(), 256),
                                                                  std::max<int64_t>(al->slot_budget, 1ll << 22) / per1));
-        al->d_scratch2.ensure((size_t)std::max<int64_t>(scratch1, 256));
+        al->d_scratch2.grow((size_t)std::max<int64_t>(scratch1, 256));
         al->d_jobs1.ensure(jobs.size());
         al->d_order1.ensure(std::max<size_t>(jobs.size(), 1));
         al->d_ctr1.ensure(2);
@@ -2976,7 +2976,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 if (!is_split[j]) queue.push_back(j);
         }
         const int nj = (int)queue.size();
-        scr.ensure((size_t)std::max<int64_t>(scratch, 256));
+        scr.grow((size_t)std::max<int64_t>(scratch, 256));  // (1.5x headroom: batches grow loop by loop)
         put(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob));
         al->d_order.grow(queue.size());
         put(al->d_order.p, queue.data(), queue.size() * 4);
@@ -3015,24 +3015,24 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // cleared only when they grow or the 16-bit epochs run out.
         const size_t tneed = as ? std::max(slots * tcap, slots1 * ((size_t)1 << tlog1)) : slots * tcap;
         if (tneed > al->tcap_alloc || al->epoch_base > 0xF000) {
-            al->tkeys.ensure(tneed);
-            al->tmask.ensure(tneed);
-            al->tdone.ensure(tneed);  // reset when a key is claimed
+            al->tkeys.grow(tneed);
+            al->tmask.grow(tneed);
+            al->tdone.grow(tneed);  // reset when a key is claimed
             NPGX_HIP(hipMemsetAsync(al->tkeys.p, 0, al->tkeys.cap * 8, st));
             NPGX_HIP(hipMemsetAsync(al->tmask.p, 0, al->tmask.cap * 8, st));  // epoch-tagged masks (vector search)
-            al->tcap_alloc = std::max(al->tcap_alloc, tneed);
+            al->tcap_alloc = std::min({al->tkeys.cap, al->tmask.cap, al->tdone.cap});  // cleared headroom counts
             al->epoch_base = 1;
         }
         zero(d_slot_epoch, 4);
         const size_t sneed = as ? std::max(slots * depth, slots1 * depth1) : slots * depth;
-        al->st_p.ensure(sneed * 64);
-        al->st_len.ensure(sneed * 64);
-        al->st_pos.ensure(sneed * 64);
-        al->st_col.ensure(sneed);
+        al->st_p.grow(sneed * 64);
+        al->st_len.grow(sneed * 64);
+        al->st_pos.grow(sneed * 64);
+        al->st_col.grow(sneed);
         const int slot_cols = (int)cols_need;
         const size_t cneed = as ? std::max(slots * (size_t)slot_cols, slots1 * (size_t)cols1) : slots * (size_t)slot_cols;
-        al->regions.ensure(cneed);
-        al->good_col.ensure(cneed);
+        al->regions.grow(cneed);
+        al->good_col.grow(cneed);
 
         pmark(4);
         SaArgs A;

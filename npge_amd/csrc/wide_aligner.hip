@@ -416,6 +416,7 @@ struct Job {
             __syncthreads();
             for (int k = 1; k < n; k++) {
                 const RowV v = F.rv[k];
+                int raised = 0;  // a row that raises no word ends the pass: none can be complete
                 for (int s0 = 0; s0 < M; s0 += 4 * WT) {
                     uint32_t hs[4];
                     unsigned long long nv[4];
@@ -437,10 +438,14 @@ struct Job {
                     __syncthreads();  // every state of the step read before its atomics
 #pragma unroll
                     for (int u = 0; u < 4; u++)
-                        if (hs[u] != ~0u) atomicMin(pt + hs[u], nv[u]);
+                        if (hs[u] != ~0u) {
+                            atomicMin(pt + hs[u], nv[u]);
+                            raised = 1;
+                        }
                     __threadfence();
                     __syncthreads();
                 }
+                if (!__syncthreads_or(raised)) break;
             }
             // S*: the smallest T of a word all n rows have sighted
             int tmin = 0x7fffffff;

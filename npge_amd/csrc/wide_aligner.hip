@@ -508,35 +508,57 @@ struct Job {
         // whole prefixes (prefix_search)
         const bool lng = a.lh > 0 && max_shift > a.lh;
         const int head = lng ? a.lh : max_shift;
+        // per shift: the rows' words inserted (the first RPT x WT rows' words
+        // kept in registers for the count test), one barrier, the count test
+        // with the last completing row's index raised in LDS, one barrier
+        constexpr int RPT = 4;
         for (; shift < head; shift++) {
             __syncthreads();
             if (C->n_pu + (uint32_t)n > tcap / 2 || C->n_wu + (uint32_t)n > tcap / 2) {
                 fail(1);
                 break;
             }
-            for (int i = threadIdx.x; i < n; i += WT) {
+            if (threadIdx.x == 0) C->r32 = -0x7fffffff;
+            const RowV v0 = F.rv[0];
+            const unsigned long long w0 = word_at(v0, F.dir, v0.pos + shift, ac);
+            bool same = true;
+            unsigned long long wr[RPT];
+#pragma unroll
+            for (int u = 0; u < RPT; u++) {
+                const int i = (int)threadIdx.x + u * WT;
+                wr[u] = 0;
+                if (i < n) {
+                    const RowV v = F.rv[i];
+                    wr[u] = word_at(v, F.dir, v.pos + shift, ac);
+                    same &= wr[u] == w0;
+                    if (pair_insert((wr[u] << 16) | (unsigned long long)i)) atomicAdd(wc + word_slot(wr[u], true), 1u);
+                }
+            }
+            for (int i = threadIdx.x + RPT * WT; i < n; i += WT) {
                 const RowV v = F.rv[i];
                 const unsigned long long w = word_at(v, F.dir, v.pos + shift, ac);
+                same &= w == w0;
                 if (pair_insert((w << 16) | (unsigned long long)i)) atomicAdd(wc + word_slot(w, true), 1u);
             }
             __threadfence();
             __syncthreads();
-            const RowV v0 = F.rv[0];
-            const unsigned long long w0 = word_at(v0, F.dir, v0.pos + shift, ac);
-            bool same = true;
             int cand = -1;
-            for (int i = threadIdx.x; i < n; i += WT) {
-                const RowV v = F.rv[i];
-                const unsigned long long w = word_at(v, F.dir, v.pos + shift, ac);
-                same &= w == w0;
-                if (aload(wc + word_slot(w, false)) == (uint32_t)n) cand = i;
+#pragma unroll
+            for (int u = 0; u < RPT; u++) {
+                const int i = (int)threadIdx.x + u * WT;
+                if (i < n && aload(wc + word_slot(wr[u], false)) == (uint32_t)n) cand = i;
             }
+            for (int i = threadIdx.x + RPT * WT; i < n; i += WT) {
+                const RowV v = F.rv[i];
+                if (aload(wc + word_slot(word_at(v, F.dir, v.pos + shift, ac), false)) == (uint32_t)n) cand = i;
+            }
+            if (cand >= 0) atomicMax(&C->r32, cand);  // the last row completing a word wins
             if (__syncthreads_and(same)) {  // one word: every row at this shift
                 for (int i = threadIdx.x; i < n; i += WT) F.rv[i].pad = shift;
                 found = true;
                 break;
             }
-            cand = lds_max(*C, cand);  // the last row completing a word wins
+            cand = C->r32;
             if (cand >= 0) {
                 if (threadIdx.x == (unsigned)(cand % WT)) {
                     const RowV v = F.rv[cand];
@@ -1139,9 +1161,10 @@ void align_wide(WideBufs* W, hipStream_t st, const char* d_rows, const int64_t* 
             // try_aligned's prefix search after the first WIDE_LONG_HEAD shifts
             // (NPGX_WIDE_LONG_HEAD; 0: shift by shift only, the round-4 search)
             const char* wl = getenv("NPGX_WIDE_LONG_HEAD");  // (read per batch: tests switch it)
-            const int wlh = wl && *wl ? std::max(0, atoi(wl)) : 128;
+            const int wlh = wl && *wl ? std::max(0, atoi(wl)) : 4;
             A.lh = wlh;
-            A.lm = 512;
+            const char* wm = getenv("NPGX_WIDE_LONG_M");  // the first prefix (doubling from there)
+            A.lm = wm && *wm ? std::max(1, atoi(wm)) : 512;
             hipLaunchKernelGGL(k_align_wide, dim3((unsigned)nw), dim3(WT), 0, st, A);
             NPGX_HIP(hipGetLastError());
             std::vector<int32_t> L(nw), S(nw);

@@ -310,7 +310,7 @@ def test_refine_random(seed):
             assert g == orc.align(a, mode="refine"), a
 
 
-@pytest.mark.parametrize("head", ["128", "1", "0"])
+@pytest.mark.parametrize("head", ["128", "4", "1", "0"])
 def test_wide_long_restart_searches(head, monkeypatch):
     """The wide aligner's prefix search (prefix_search, wide_aligner.hip)
     against the oracle: more than 64 rows with unrelated insertions of up to

@@ -67,26 +67,36 @@ int guard(F&& f) {
     }
 }
 
+// Device (kind 0) and pinned host (kind 1) allocations, optionally through a
+// cache of freed buffers (NPGX_BUF_CACHE=1; seqset.hip: size classes, one
+// device synchronisation before freed buffers are reused, reused device
+// buffers zeroed).  buf_alloc sets *got to the bytes actually held (what
+// buf_free takes back).
+void* buf_alloc(int kind, size_t bytes, size_t* got);
+void buf_free(int kind, void* p, size_t got);
+
 // Growable device buffer (capacity kept across runs so repeated steps do not
 // re-allocate).
 template <class T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;
+    size_t held = 0;  // bytes of the allocation
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { release(); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) buf_free(0, p, held);
         p = nullptr;
         cap = 0;
+        held = 0;
     }
     T* ensure(size_t n) {
         if (n == 0) n = 1;
         if (n > cap) {
             release();
-            NPGX_HIP(hipMalloc(&p, n * sizeof(T)));
+            p = (T*)buf_alloc(0, n * sizeof(T), &held);
             cap = n;
         }
         return p;
@@ -100,19 +110,20 @@ template <class T>
 struct PinnedBuf {
     T* p = nullptr;
     size_t cap = 0;
+    size_t held = 0;
     PinnedBuf() = default;
     PinnedBuf(const PinnedBuf&) = delete;
     PinnedBuf& operator=(const PinnedBuf&) = delete;
     ~PinnedBuf() {
-        if (p) (void)hipHostFree(p);
+        if (p) buf_free(1, p, held);
     }
     T* ensure(size_t n) {
         if (n == 0) n = 1;
         if (n > cap) {
-            if (p) (void)hipHostFree(p);
+            if (p) buf_free(1, p, held);
             p = nullptr;
             cap = std::max(n, cap + cap / 2);
-            NPGX_HIP(hipHostMalloc((void**)&p, cap * sizeof(T), hipHostMallocDefault));
+            p = (T*)buf_alloc(1, cap * sizeof(T), &held);
         }
         return p;
     }
@@ -122,12 +133,12 @@ struct PinnedBuf {
 // is synchronised so every earlier copy from it has completed).
 struct PinnedArena {
     char* p = nullptr;
-    size_t cap = 0, used = 0;
+    size_t cap = 0, used = 0, held = 0;
     PinnedArena() = default;
     PinnedArena(const PinnedArena&) = delete;
     PinnedArena& operator=(const PinnedArena&) = delete;
     ~PinnedArena() {
-        if (p) (void)hipHostFree(p);
+        if (p) buf_free(1, p, held);
     }
     char* take(size_t n, hipStream_t st) {
         n = (n + 63) & ~(size_t)63;
@@ -135,10 +146,10 @@ struct PinnedArena {
             NPGX_HIP(stream_wait(st));
             used = 0;
             if (n > cap) {
-                if (p) (void)hipHostFree(p);
+                if (p) buf_free(1, p, held);
                 p = nullptr;
                 cap = std::max<size_t>(std::max<size_t>(n, 2 * cap), (size_t)1 << 22);
-                NPGX_HIP(hipHostMalloc((void**)&p, cap, hipHostMallocDefault));
+                p = (char*)buf_alloc(1, cap, &held);
             }
         }
         char* r = p + used;

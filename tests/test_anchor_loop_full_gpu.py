@@ -94,3 +94,30 @@ def test_processor_mirror():
     o.set_blocks(blocks)
     o.apply("AddingLoopBySize")
     assert not other.blocks and got == canon(o.blocks())
+
+
+def test_anchor_loop_failure_keeps_blocks(monkeypatch):
+    """A failure inside AnchorLoop while the set's own blocks wait aside
+    (after the first DeConSeq; NPGX_TEST_FAIL_ANCHOR_LOOP=1 injects it): the
+    call reports the error and the set holds its own blocks as the pipe's
+    first steps left them (Filter, then Rest: lua_lib.lua:711-737 applies the
+    processors to the target one by one), not the deconseq list it was
+    working on; the handle then runs the pipe again."""
+    from npge_amd.anchor_finder import AnchorFinder
+    names, seqs = synth.genome_set("tiny")
+    o = orc.BlockSetOracle(seqs, names)
+    o.apply("DraftPangenome")
+    start = o.blocks()
+    eng = _engine(seqs, names, start)
+    monkeypatch.setenv("NPGX_TEST_FAIL_ANCHOR_LOOP", "1")
+    with pytest.raises(Exception, match="injected failure"):
+        eng.apply("AnchorLoop", af=AnchorFinder())
+    o.set_blocks(start)
+    o.apply("Filter")
+    o.apply("Rest")
+    mid = o.blocks()
+    assert canon(eng.blocks()) == canon(mid)
+    monkeypatch.delenv("NPGX_TEST_FAIL_ANCHOR_LOOP")
+    eng.apply("AnchorLoop", af=AnchorFinder())
+    o.apply("AnchorLoop")
+    assert canon(eng.blocks()) == canon(o.blocks())

@@ -218,6 +218,10 @@ def main():
 
     if roofline is not None:
         roofline.update(pmc_traffic(dom["name"], args.config))
+    # stage accounting from one extra, untimed step with HIP events at the
+    # stage boundaries (markers cost the GPU time: never in the timed region)
+    stages = job.stage_timeline()
+    stages["ms_per_step"] = round(dt / args.steps * 1e3, 4)
     workload = job.workload_name(args.config)
     del job
 
@@ -307,6 +311,7 @@ def main():
                                                                        args.dist_backend)) if sharded
                        else "replica-per-gpu x%d (independent sets, no data-path collective)" % world},
             "last_step": info,
+            "stage_timeline": stages,
             "kernels_last_step": kernels,
             "roofline": roofline,
             "pcie_inclusive": pcie,

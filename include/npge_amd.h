@@ -328,7 +328,9 @@ typedef struct {
     /* wall ms per stage of the last apply: 0 AnchorFinder, 1 RemoveNonStem +
      * DummyAligner, 2 MoveUnchanged, 3 flank gather, 4 align batch, 5 stitch,
      * 6 FixEnds, 7 OverlaplessUnion, 8 blockset hash, 9 Filter,
-     * 10 aligner host preparation, 11 aligner kernel wait, 12 FixEnds
+     * 10 aligner host preparation, 11 the host's waits on the device (the
+     * aligner's kernels in the host loop; each iteration's GPU work in the
+     * device loop, whose other entries are then enqueue times), 12 FixEnds
      * device part, 13 FixEnds slicing, 14 OverlaplessUnion order,
      * 15 OverlaplessUnion admission */
     double ms_stage[16];
@@ -354,6 +356,24 @@ typedef struct {
      * ExtendAndAlign (FragmentsExtender + Align), 5 ExtendLoopFast, 6 DeConSeq,
      * 7 the closing Align (the consensus pipe's stages add into ms_stage) */
     double ms_loop[8];
+    /* DraftPangenome's GPU timeline with the "stage-clock" tuning on (else 0):
+     * ms between HIP events recorded on the set's stream at the stage
+     * boundaries, so the entries sum to the step's span on the GPU (kernels
+     * plus the idle time the host leaves between them): 0 AnchorFinder (its
+     * kernels, grouping, anchor blocks), 1 RemoveNonStem + DummyAligner, 2
+     * ExtendLoopFast table upload, 3 per iteration: block_hash, Pipe state,
+     * MoveUnchanged, flank plan + its download and the host's batch arrays,
+     * 4 flank decode, 5 aligner (k_align_jobs and its re-runs / sub-jobs),
+     * 6 stitch, 7 FixEnds + slicing, 8 OverlaplessUnion, 9 the blocks'
+     * download, 10 Filter, 11 ExtendLoopFast on the host (host loop only) */
+    double ms_gpu[12];
+    /* ExtendLoopFast iterations the device loop ran (ms_align and ms_stage 3-8
+     * are then host enqueue times: the GPU time is in ms_gpu) */
+    int64_t device_iterations;
+    /* ... of which the aligner ran synchronously because the asynchronous
+     * form's planned memory passed its budget (NPGX_ASYNC_BUDGET_MB) or a
+     * problem had more than 64 rows */
+    int64_t device_sync_iterations;
 } npgx_bb_stats;
 
 void npgx_bb_default_options(npgx_bb_options* o);
@@ -373,7 +393,12 @@ int npgx_blockset_create_sharing(const npgx_seqset* s, const npgx_bb_options* o,
  *                streams, e.g. the pair job).  Sets sharing the aligner share it.
  *   "elf-device" ExtendLoopFast on the device (1), on the host (0) or the
  *                default (-1, the device where its rules allow); sets made by
- *                npgx_blockset_create_sharing inherit the lender's.
+ *                npgx_blockset_create_sharing inherit the lender's, and so do
+ *                the sets a pipe makes internally (AnchorLoopFast's and
+ *                AnchorLoop's consensus sets).
+ *   "stage-clock" 1: DraftPangenome records HIP events at its stage
+ *                boundaries and fills npgx_bb_stats.ms_gpu (each marker costs
+ *                the GPU a few microseconds: diagnostics only); 0: off (default).
  * NPGX_ERR_ARG for an unknown key or a value out of range. */
 int npgx_blockset_tune(npgx_blockset* b, const char* key, int64_t value);
 /* replace the blocks; row_off == NULL: no rows, else row i = rows[row_off[i]..row_off[i+1])

@@ -30,12 +30,16 @@ class BbStats(ctypes.Structure):
                 ("stem_blocks", ctypes.c_int64), ("ms_align", ctypes.c_double),
                 ("ms_host", ctypes.c_double), ("ms_stage", ctypes.c_double * 16),
                 ("counters", ctypes.c_int64 * 8), ("loop", ctypes.c_int64 * 8),
-                ("ms_loop", ctypes.c_double * 8)]
+                ("ms_loop", ctypes.c_double * 8), ("ms_gpu", ctypes.c_double * 12),
+                ("device_iterations", ctypes.c_int64), ("device_sync_iterations", ctypes.c_int64)]
 
 STAGE_NAMES = ["anchor_finder", "stem_dummy", "move_unchanged", "flank_gather", "align_batch",
                "stitch", "fix_ends", "overlapless_union", "blockset_hash", "filter",
-               "align_host_prep", "align_kernel_wait", "fix_ends_device", "fix_ends_slice",
+               "align_host_prep", "device_wait", "fix_ends_device", "fix_ends_slice",
                "ou_order", "ou_admit"]
+# npgx_bb_stats.ms_gpu: DraftPangenome's GPU timeline by stage ("stage-clock" tuning)
+GPU_STAGE_NAMES = ["anchor_finder", "stem_dummy", "elf_upload", "elf_plan", "flank_decode", "align", "stitch",
+                   "fix_ends", "overlapless_union", "elf_download", "filter", "extend_loop_host"]
 JOB_STATS = 24  # NPGX_JOB_STATS
 COUNTER_NAMES = ["blocks_after_extend", "filter_whole", "filter_slices", "blocks_after_filter",
                  "ou_in", "ou_rejected", "hashes", "spare"]
@@ -223,7 +227,8 @@ class BlockSetEngine:
         """npgx_blockset_tune: "long-head" (the aligner's incremental shifts
         before the prefix search; 0 = never, the low-scratch kernels) or
         "elf-device" (1 / 0 / -1: ExtendLoopFast on the device / host /
-        default).  Results do not change."""
+        default) or "stage-clock" (1: DraftPangenome fills stats()["ms_gpu"],
+        its GPU timeline by stage).  Results do not change."""
         _capi.check(_capi.lib().npgx_blockset_tune(self._h, key.encode(), ctypes.c_int64(int(value))))
         return self
 
@@ -243,7 +248,8 @@ class BlockSetEngine:
         st = BbStats()
         _capi.check(_capi.lib().npgx_blockset_stats(self._h, ctypes.byref(st)))
         d = {k: getattr(st, k) for k, _ in BbStats._fields_
-             if k not in ("ms_stage", "counters", "loop", "ms_loop")}
+             if k not in ("ms_stage", "counters", "loop", "ms_loop", "ms_gpu")}
+        d["ms_gpu"] = {n: round(st.ms_gpu[i], 3) for i, n in enumerate(GPU_STAGE_NAMES)}
         d["ms_stage"] = {n: round(st.ms_stage[i], 3) for i, n in enumerate(STAGE_NAMES)}
         d["counters"] = {n: int(st.counters[i]) for i, n in enumerate(COUNTER_NAMES)}
         d["loop"] = {n: int(st.loop[i]) for i, n in enumerate(LOOP_NAMES)}

@@ -499,7 +499,7 @@ __global__ void k_table_insert(const uint64_t* __restrict__ hs, int64_t n, Table
                       (unsigned long long)h);
         if (prev == EMPTY_KEY) {
             slots[s].val = (uint32_t)i;
-            slots[s].pad = 0u;  // the slot's FoundFragment count (k_ff_count)
+            slots[s].pad = 0u;
             atomicOr(&occ[s >> 5], 1u << (s & 31));
             return;
         }
@@ -507,22 +507,9 @@ __global__ void k_table_insert(const uint64_t* __restrict__ hs, int64_t n, Table
     }
 }
 
-// the slot of h, or -1 (table_find, returning where the key sits)
-__device__ __forceinline__ int64_t table_slot(const TableArgs& t, uint64_t h) {
-    uint32_t s = (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> t.shift) & t.mask;
-    if (!((t.occ[s >> 5] >> (s & 31)) & 1u)) return -1;
-    while (true) {
-        const uint64_t key = t.slots[s].key;
-        if (key == h) return (int64_t)s;
-        if (key == EMPTY_KEY) return -1;
-        s = (s + 1) & t.mask;
-    }
-}
-
-// counts: per hash index (atomics on counts[]), or, with counts == null, in
-// the slot itself (TableSlot.pad: the cache line the key compare just read,
-// instead of a second random line per member window; k_slot_counts gathers
-// them into counts[])
+// FoundFragment counts per hash index (atomics on counts[]).  (Round 5 tried
+// the counts in the membership table's slots, the cache line the key compare
+// just read: no faster at C3 / C5, profiles/r05j_af_slot_counts.txt; removed.)
 __global__ __launch_bounds__(WG) void k_ff_count(AfArgs a, TableArgs t, uint32_t* __restrict__ counts) {
     const Chunk c = a.chunks[blockIdx.x];
     const SeqMeta s = a.meta[c.seq];
@@ -532,21 +519,8 @@ __global__ __launch_bounds__(WG) void k_ff_count(AfArgs a, TableArgs t, uint32_t
     if (!load_window(a, s, p, dir)) return;
     const uint64_t rev = revcomp(dir, a.k);
     const uint64_t h = dir < rev ? dir : rev;
-    if (!counts) {
-        const int64_t sl = table_slot(t, h);
-        if (sl >= 0) atomicAdd(&((TableSlot*)t.slots)[sl].pad, 1u);
-        return;
-    }
     const int64_t idx = table_find(t, h);
     if (idx >= 0) atomicAdd(&counts[idx], 1u);
-}
-
-// the slots' counts into counts[] by hash index (one coalesced pass over the table)
-__global__ void k_slot_counts(const TableSlot* __restrict__ slots, uint64_t cap, uint32_t* __restrict__ counts) {
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
-        const TableSlot x = slots[s];
-        if (x.key != EMPTY_KEY) counts[x.val] = x.pad;
-    }
 }
 
 __global__ void k_find_cut(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ counts,
@@ -1093,15 +1067,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
 
         // --- pass 2a: FoundFragment counts per hash
         ti = af->timer.begin("ff_count", st, local_windows * (0.375 + 12.0), local_windows);
-        // the counts by atomics on counts[] (NPGX_AF_SLOT_COUNT=1: the counts in the membership table's slots; measured no faster at C3 / C5,
-        // profiles/r05j_af_slot_counts.txt)
-        static const bool slot_count = getenv("NPGX_AF_SLOT_COUNT") && getenv("NPGX_AF_SLOT_COUNT")[0] == '1';
-        if (run_local) {
-            hipLaunchKernelGGL(k_ff_count, grid, block, 0, st, A, T, slot_count ? nullptr : af->counts.p);
-            if (slot_count)
-                hipLaunchKernelGGL(k_slot_counts, dim3((unsigned)std::min<uint64_t>(4096, (cap + 255) / 256)), dim3(256),
-                                   0, st, af->tslots.p, (uint64_t)cap, af->counts.p);
-        }
+        if (run_local) hipLaunchKernelGGL(k_ff_count, grid, block, 0, st, A, T, af->counts.p);
         NPGX_HIP(hipGetLastError());
         af->timer.end(ti, st);
         if (comm) {

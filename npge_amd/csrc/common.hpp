@@ -103,6 +103,11 @@ struct DevBuf {
     }
     // ensure() with 1.5x headroom for buffers whose size varies from call to call
     T* grow(size_t n) { return ensure(n > cap ? std::max(n, cap + cap / 2) : n); }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+        std::swap(held, o.held);
+    }
 };
 
 // Pinned host buffer that only grows.
@@ -228,6 +233,51 @@ struct StageTimer {
         }
         *n = (int32_t)recs.size();
         return NPGX_OK;
+    }
+};
+
+// Step timeline: one HIP event at each stage boundary of a step on one stream;
+// the interval ending at a marker is booked to that marker's stage, so the
+// stages sum to the step's GPU-timeline span (device time plus the idle time
+// the host leaves between them).  Off unless a caller turns it on: every
+// marker is a queue packet that costs the GPU a few microseconds (bench.py
+// runs one extra, untimed step with it).
+struct StageClock {
+    bool on = false;
+    bool live = false;  // between start() and collect()
+    std::vector<std::pair<hipEvent_t, int>> marks;
+    std::vector<hipEvent_t> pool;
+    ~StageClock() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+    void start(hipStream_t s) {
+        marks.clear();
+        live = on;
+        mark(s, -1);
+    }
+    void mark(hipStream_t s, int stage) {
+        if (!live) return;
+        if (marks.size() == pool.size()) {
+            hipEvent_t e;
+            NPGX_HIP(hipEventCreate(&e));
+            pool.push_back(e);
+        }
+        hipEvent_t e = pool[marks.size()];
+        NPGX_HIP(hipEventRecord(e, s));
+        marks.emplace_back(e, stage);
+    }
+    // out[stage] += ms of every interval; the caller has waited for the work
+    void collect(double* out, int nstages) {
+        if (!live) return;
+        live = false;
+        for (size_t i = 1; i < marks.size(); i++) {
+            float ms = 0.f;
+            NPGX_HIP(hipEventSynchronize(marks[i].first));
+            NPGX_HIP(hipEventElapsedTime(&ms, marks[i - 1].first, marks[i].first));
+            const int k = marks[i].second;
+            if (k >= 0 && k < nstages) out[k] += ms;
+        }
+        marks.clear();
     }
 };
 

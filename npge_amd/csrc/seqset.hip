@@ -203,12 +203,25 @@ void raw_free(int kind, void* p) {
 hipError_t raw_alloc(int kind, void** p, size_t bytes) {
     return kind == 0 ? hipMalloc(p, bytes) : hipHostMalloc(p, bytes, hipHostMallocDefault);
 }
-// the pending buffers of device dev become reusable (caller holds the lock)
+// the pending buffers of device dev (-1: the pinned host buffers) become
+// reusable once that device (every device, for pinned buffers, which any
+// device's copies may still read) has finished its work (caller holds the lock)
 void buf_flush(BufCache& c, int dev) {
     bool any = false;
     for (const auto& e : c.pend) any |= std::get<1>(e.first) == dev;
     if (!any) return;
-    NPGX_HIP(hipDeviceSynchronize());
+    if (dev >= 0) {
+        DeviceGuard g(dev);
+        NPGX_HIP(hipDeviceSynchronize());
+    } else {
+        int nd = 0;
+        NPGX_HIP(hipGetDeviceCount(&nd));
+        for (int d = 0; d < nd; d++) {
+            DeviceGuard g(d);
+            NPGX_HIP(hipDeviceSynchronize());
+        }
+    }
+    DeviceGuard g(dev >= 0 ? dev : 0);  // (the zeroing below runs on the buffers' own device)
     bool zeroed = false;
     std::vector<std::pair<BufCache::Key, void*>> keep;
     for (const auto& e : c.pend) {
@@ -238,8 +251,8 @@ void* buf_alloc(int kind, size_t bytes, size_t* got) {
     BufCache& c = buf_cache();
     const size_t cls = c.on ? buf_class(bytes) : bytes;  // (off: the exact size, as before)
     *got = cls;
-    int dev = 0;
-    NPGX_HIP(hipGetDevice(&dev));
+    int dev = -1;  // pinned host buffers are filed under -1: any device may use them
+    if (kind == 0) NPGX_HIP(hipGetDevice(&dev));
     void* p = nullptr;
     if (c.on) {
         std::lock_guard<std::mutex> lk(c.mu);
@@ -265,6 +278,7 @@ void* buf_alloc(int kind, size_t bytes, size_t* got) {
         (void)hipGetLastError();
         std::lock_guard<std::mutex> lk(c.mu);
         buf_flush(c, dev);
+        if (kind == 0) NPGX_HIP(hipSetDevice(dev));
         for (auto it = c.ready.begin(); it != c.ready.end();) {
             if (std::get<0>(it->first) == kind && std::get<1>(it->first) == dev) {
                 raw_free(kind, it->second);
@@ -283,8 +297,20 @@ void* buf_alloc(int kind, size_t bytes, size_t* got) {
 void buf_free(int kind, void* p, size_t cls) {
     if (!p) return;
     BufCache& c = buf_cache();
-    int dev = 0;
-    if (c.on && hipGetDevice(&dev) == hipSuccess) {
+    // filed under the device that owns the allocation, not the calling
+    // thread's current device (a set freed from another device's thread)
+    int dev = -1;
+    bool known = kind == 1;
+    if (c.on && kind == 0) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, p) == hipSuccess && a.device >= 0) {
+            dev = a.device;
+            known = true;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    if (c.on && known) {
         std::lock_guard<std::mutex> lk(c.mu);
         if (c.held[kind] + cls <= BUF_CACHE_MAX[kind]) {
             c.pend.emplace_back(BufCache::Key{kind, dev, cls}, p);

@@ -263,9 +263,9 @@ class PairJobs:
                 "aligned_residues": int(sum(i["aligned_residues"] for i in done)),
                 "align_jobs": int(sum(i["align_jobs"] for i in done)),
                 # one pair's engine timings, averaged (wall clock of its own thread)
-                "mean_pair_ms": {k: round(sum(i["ms_stage"][k] for i in done) / max(len(done), 1), 3)
-                                 for k in (done[0]["ms_stage"] if done else {})},
-                "mean_pair_ms_align": round(sum(i["ms_align_wall"] for i in done) / max(len(done), 1), 3),
+                "mean_pair_ms": {k: round(sum(i["ms_stage_host"][k] for i in done) / max(len(done), 1), 3)
+                                 for k in (done[0]["ms_stage_host"] if done else {})},
+                "mean_pair_ms_align": round(sum(i.get("ms_align_wall", 0.0) for i in done) / max(len(done), 1), 3),
                 "mean_pair_ms_host": round(sum(i["ms_host_bookkeeping"] for i in done) / max(len(done), 1), 3)}
 
     def hashes(self):

@@ -59,11 +59,35 @@ class BlockBuild:
             self._extra_kt = draft_kt + self.loop_af.kernel_times()
         else:
             self._extra_kt = []
-        return {"anchor_blocks": int(st["anchor_blocks"]), "stem_blocks": int(st["stem_blocks"]),
-                "iterations": int(st["iterations"]), "aligned_residues": int(st["aligned_residues"]),
-                "align_jobs": int(st["align_jobs"]), "ms_align_wall": round(st["ms_align"], 3),
-                "ms_host_bookkeeping": round(st["ms_host"], 3), "ms_stage": st["ms_stage"],
-                "counters": st["counters"], "anchor_loop": loop}
+        out = {"anchor_blocks": int(st["anchor_blocks"]), "stem_blocks": int(st["stem_blocks"]),
+               "iterations": int(st["iterations"]), "aligned_residues": int(st["aligned_residues"]),
+               "align_jobs": int(st["align_jobs"]), "device_loop": st["device_iterations"] > 0,
+               "ms_host_bookkeeping": round(st["ms_host"], 3), "ms_stage_host": st["ms_stage"],
+               "counters": st["counters"], "anchor_loop": loop}
+        if not out["device_loop"]:  # (the device loop's is the aligner's enqueue time: see stage_timeline)
+            out["ms_align_wall"] = round(st["ms_align"], 3)
+        return out
+
+    def stage_timeline(self):
+        """One extra DraftPangenome with the engine's stage clock on (HIP events
+        at the stage boundaries on its stream; each costs the GPU a few
+        microseconds, so callers run it outside any timed region): the step's
+        GPU timeline by stage, which sums to the step's span, and the wall
+        time of that step."""
+        import time
+        self.eng.tune("stage-clock", 1)
+        try:
+            self.af.clear_used()
+            t = time.perf_counter()
+            self.eng.apply("DraftPangenome", af=self.af)
+            wall = (time.perf_counter() - t) * 1e3
+        finally:
+            self.eng.tune("stage-clock", 0)
+        ms = self.eng.stats()["ms_gpu"]
+        return {"ms": ms, "sum_ms": round(sum(ms.values()), 3), "step_wall_ms": round(wall, 3),
+                "largest": max(ms, key=ms.get),
+                "source": "HIP events at the stage boundaries of one extra untimed DraftPangenome step "
+                          "(npgx_blockset_tune stage-clock; intervals include the idle time the host leaves)"}
 
     def kernel_times(self):
         """Per-kernel totals of the last step: name -> (ms, bytes, launches)."""

@@ -90,13 +90,11 @@ def _draft(cfg, device, monkeypatch):
     return eng.blocks(), eng.rows_digest(), st
 
 
-@pytest.mark.parametrize("scan", ["0", "1"])
-def test_ou_device_multi_launch_passes(scan, monkeypatch):
-    """The table passes in their many-workgroup forms (tables of more than
-    2048 blocks take them; NPGX_ELF_PASS_WG=0 forces them here): the look-back
-    launch, or (scan=1) count / device-wide scan / fill launches."""
+def test_ou_device_multi_launch_passes(monkeypatch):
+    """The table passes in their many-workgroup form (tables of more than
+    2048 blocks take it; NPGX_ELF_PASS_WG=0 forces it here): one launch with
+    decoupled look-back over 256-block tiles."""
     monkeypatch.setenv("NPGX_ELF_PASS_WG", "0")
-    monkeypatch.setenv("NPGX_ELF_PASS_SCAN", scan)
     rng = np.random.default_rng(31)
     n_seqs, seq_len = 6, 300000
     seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
@@ -110,16 +108,14 @@ def test_ou_device_multi_launch_passes(scan, monkeypatch):
     assert eng.blocks() == o.blocks()
 
 
-@pytest.mark.parametrize("cfg,only,scan", [("tiny", p, "0") for p in ("plan", "stitch", "fix_ends_plan", "slice",
-                                                                       "ou_prep", "ou_scan", "ou_compact")]
-                         + [("tiny", "", "0"), ("rtiny", "", "0"), ("tiny", "", "1"), ("rtiny", "", "1")])
-def test_draft_device_multi_launch_passes(cfg, only, scan, monkeypatch):
+@pytest.mark.parametrize("cfg,only", [("tiny", p) for p in ("plan", "stitch", "fix_ends_plan", "slice",
+                                                            "ou_prep", "ou_scan", "ou_compact")]
+                         + [("tiny", ""), ("rtiny", "")])
+def test_draft_device_multi_launch_passes(cfg, only, monkeypatch):
     """Every table pass (or one, `only`) in its many-workgroup form: one
-    launch with decoupled look-back over 256-block tiles, or (scan=1) count /
-    rocPRIM scan / fill launches."""
+    launch with decoupled look-back over 256-block tiles."""
     monkeypatch.setenv("NPGX_ELF_PASS_WG", "0")
     monkeypatch.setenv("NPGX_ELF_PASS_MULTI", only)
-    monkeypatch.setenv("NPGX_ELF_PASS_SCAN", scan)
     b_dev, d_dev, s_dev = _draft(cfg, True, monkeypatch)
     b_host, d_host, s_host = _draft(cfg, False, monkeypatch)
     assert canon(b_dev) == canon(b_host)
@@ -201,3 +197,78 @@ def test_blockset_tune(monkeypatch):
     for k, v in (("no-such-key", 1), ("elf-device", 2), ("long-head", -1)):
         with pytest.raises(_capi.NpgxError):
             eng.tune(k, v)
+
+
+@pytest.mark.parametrize("fail_iter", [0, 1, 2])
+def test_extend_loop_fast_device_failure_keeps_blocks(fail_iter, monkeypatch):
+    """A failure inside the device loop (injected after iteration k's stitch:
+    the first stitch wrote the other row buffer, the later ones would have
+    overwritten the entry rows) leaves the set with its blocks and rows as
+    they came in; the handle then runs the loop to the oracle's result."""
+    from npge_amd import _capi
+    monkeypatch.setenv("NPGX_ELF_DEVICE", "1")
+    names, seqs = synth.genome_set("small")
+    b0 = _stem_blocks(seqs, names)
+    ss, eng = _engine(seqs, names, max_iterations=6)
+    eng.set_blocks(b0).apply("DummyAligner")
+    before, d_before = canon(eng.blocks()), eng.rows_digest()
+    monkeypatch.setenv("NPGX_TEST_FAIL_ELF", str(fail_iter))
+    with pytest.raises(_capi.NpgxError, match="injected"):
+        eng.apply("ExtendLoopFast")
+    assert canon(eng.blocks()) == before
+    assert eng.rows_digest() == d_before
+    monkeypatch.delenv("NPGX_TEST_FAIL_ELF")
+    eng.apply("ExtendLoopFast")
+    o = orc.BlockSetOracle(seqs, names, max_iterations=6)
+    o.set_blocks(b0)
+    o.apply("DummyAligner")
+    o.apply("ExtendLoopFast")
+    assert canon(eng.blocks()) == canon(o.blocks())
+    assert eng.hash() == o.hash()
+
+
+def _many_rows_set(n_genomes=40, length=30000, div=0.004, seed=77):
+    """A family of n_genomes close copies of one root: blocks of ~n_genomes
+    rows whose flanks grow with their blocks (portion 0.5)."""
+    rng = np.random.default_rng(seed)
+    root = rng.integers(0, 4, size=length)
+    seqs = []
+    for g in range(n_genomes):
+        s = root.copy()
+        m = rng.random(length) < div
+        s[m] = (s[m] + rng.integers(1, 4, size=int(m.sum()))) % 4
+        seqs.append("".join("ACGT"[c] for c in s))
+    return ["f%d&c&c" % g for g in range(n_genomes)], seqs
+
+
+@pytest.mark.parametrize("budget_mb", ["0", "1"])
+def test_extend_loop_fast_device_async_budget(budget_mb, monkeypatch):
+    """The asynchronous aligner plans every job's re-run at the proven bound
+    (3 n Σlen bytes) and the stitch arena at n Σlen: past NPGX_ASYNC_BUDGET_MB
+    an iteration takes the synchronous aligner instead.  Many rows and long
+    flanks, budgets that force the fallback in every iteration (0) or in the
+    late ones (1 MiB): the result equals the default budget's, the host
+    loop's and the oracle's."""
+    from npge_amd.anchor_finder import AnchorFinder
+    names, seqs = _many_rows_set()
+    res = []
+    for dev, budget in (("1", None), ("1", budget_mb), ("0", None)):
+        monkeypatch.setenv("NPGX_ELF_DEVICE", dev)
+        if budget is None:
+            monkeypatch.delenv("NPGX_ASYNC_BUDGET_MB", raising=False)
+        else:
+            monkeypatch.setenv("NPGX_ASYNC_BUDGET_MB", budget)
+        ss, eng = _engine(seqs, names)
+        eng.apply("DraftPangenome", af=AnchorFinder())
+        st = eng.stats()
+        res.append((canon(eng.blocks()), eng.rows_digest(), st["iterations"], st["device_iterations"],
+                    st["device_sync_iterations"]))
+    assert res[0][:3] == res[1][:3] == res[2][:3]
+    assert res[0][3] > 0 and res[0][4] == 0      # the default budget: every iteration asynchronous
+    assert res[1][4] > 0                         # the small budget: the synchronous fallback ran
+    if budget_mb == "0":
+        assert res[1][4] >= res[1][3] - 1        # (an iteration without jobs has no aligner)
+    assert res[2][3] == 0
+    o = orc.BlockSetOracle(seqs, names)
+    o.apply("DraftPangenome")
+    assert canon(o.blocks()) == res[0][0]

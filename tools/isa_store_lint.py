@@ -43,16 +43,24 @@ def lint(src, out_dir):
     return hits
 
 
-def main():
-    srcs = sys.argv[1:] or sorted(glob.glob(os.path.join(REPO, "npge_amd", "csrc", "*.hip")))
-    bad = 0
+def lint_all(srcs=None, jobs=8):
+    """{source basename: [(function, asm line, store)]} over the sources
+    (default: every npge_amd/csrc/*.hip), compiled in parallel."""
+    from concurrent.futures import ThreadPoolExecutor
+    srcs = srcs or sorted(glob.glob(os.path.join(REPO, "npge_amd", "csrc", "*.hip")))
     with tempfile.TemporaryDirectory() as d:
-        for s in srcs:
-            hits = lint(s, d)
-            print("%s: %d overlapping stores" % (os.path.basename(s), len(hits)))
-            for h in hits:
-                print("   %s (line %d): %s" % h)
-            bad += len(hits)
+        with ThreadPoolExecutor(max(1, jobs)) as ex:
+            res = list(ex.map(lambda s: lint(s, d), srcs))
+    return {os.path.basename(s): h for s, h in zip(srcs, res)}
+
+
+def main():
+    bad = 0
+    for name, hits in lint_all(sys.argv[1:] or None).items():
+        print("%s: %d overlapping stores" % (name, len(hits)))
+        for h in hits:
+            print("   %s (line %d): %s" % h)
+        bad += len(hits)
     sys.exit(1 if bad else 0)
 
 

@@ -46,6 +46,7 @@ struct Params {
     int wf;  // FindLowSimilar weight factor (FindLowSimilar.cpp:56-60)
     int lh;  // try_aligned: shifts searched incrementally before the prefix search (0: never switch)
     int lm;  // ... the prefix search's first prefix (shifts)
+    int llds = 1;  // the prefix search's first prefixes in the LDS word table when they fit (NPGX_LONG_LDS)
 };
 
 // Per-wave scratch (global memory), sized by the host for the batch.
@@ -162,6 +163,26 @@ __device__ __forceinline__ void cm_copy(const WaveCtx& w, const char* src, char*
         for (int u = 0; u < 4; u++) {
             const int p = p0 + u, r = p / max(nch, 1), j = (p - r * nch) * 64 + w.lane;
             t[u] = (p < np && j < len) ? src[(size_t)r * cap + s0 + j] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = p0 + u, r = p / max(nch, 1), j = (p - r * nch) * 64 + w.lane;
+            if (p < np && j < len) dst[(size_t)r * cap + d0 + j] = t[u];
+        }
+    }
+    __syncthreads();
+}
+
+// rows [0,n): dst[d0 + j] = src[len - 1 - j] for j < len (a reversed copy;
+// src and dst rows of stride cap, (row, 64-column chunk) pairs four at a time)
+__device__ __forceinline__ void cm_copy_rev(const WaveCtx& w, const char* src, char* dst, int cap, int d0, int len) {
+    const int nch = (len + 63) >> 6, np = w.n * nch;
+    for (int p0 = 0; p0 < np; p0 += 4) {
+        char t[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = p0 + u, r = p / max(nch, 1), j = (p - r * nch) * 64 + w.lane;
+            t[u] = (p < np && j < len) ? src[(size_t)r * cap + len - 1 - j] : 0;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -520,6 +541,7 @@ typedef __attribute__((address_space(3))) unsigned char LdsU8;
 struct LongOut {
     int found, my_shift, shifts;  // found: 1, 0 (no shift works), -1 (the table cannot take a prefix)
     uint32_t epoch;
+    int M;                        // found == -1: the prefix the table could not take
 };
 
 // codes of chars q0 .. q0 + 575 of a row into LDS (7 past the row's end)
@@ -544,6 +566,12 @@ __device__ __forceinline__ void lw_words(const LdsU8* buf, int lane, int ac, uns
     }
 }
 
+// T: the table in global memory (unsigned long long) or in LDS (LdsU64: the
+// prefixes that fit the workgroup's LDS word table -- no HBM traffic, LDS
+// atomics); a call on the LDS table that meets a prefix too long for it
+// returns found -1 with that prefix in M, and the caller goes on from there
+// on the global table (every prefix's pass starts from scratch: the same answer)
+template <class TT>
 #ifdef SA_LONG_INLINE  // (A/B builds: inlined instead of called)
 __device__ __forceinline__
 #else
@@ -551,7 +579,7 @@ __device__ __noinline__
 #endif
 LongOut find_word_long(const char* vp, int vlen, int vd, int pos, int lane, int n, int ac,
                                                int max_shift, int M0, unsigned long long* W,
-                                               unsigned long long* tkeys, unsigned long long* tmask,
+                                               TT* tkeys, TT* tmask,
                                                uint32_t tcap_log2, uint32_t epoch) {
     n = __builtin_amdgcn_readfirstlane(n);
     ac = __builtin_amdgcn_readfirstlane(ac);
@@ -560,7 +588,7 @@ LongOut find_word_long(const char* vp, int vlen, int vd, int pos, int lane, int 
     tcap_log2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)tcap_log2);
     epoch = (uint32_t)__builtin_amdgcn_readfirstlane((int)epoch);
     LdsU8* buf = (LdsU8*)W;
-    LongOut out{0, 0, max_shift, epoch};
+    LongOut out{0, 0, max_shift, epoch, 0};
     const bool act = lane < n;
     const View v{vp, vlen, vd};
     const unsigned long long wmask = (ac >= 16) ? ((1ull << 48) - 1) : ((1ull << (3 * ac)) - 1);
@@ -573,6 +601,7 @@ LongOut find_word_long(const char* vp, int vlen, int vd, int pos, int lane, int 
         const int Mp = min(M, max_shift);
         if (2u * (uint32_t)Mp > tcap) {
             out.found = -1;
+            out.M = M;
             return out;
         }
         uint32_t ep32 = out.epoch + 1;
@@ -1068,9 +1097,20 @@ struct ProcT {
                 if (g != 0 || !lng) return g == 1;
             }
         }
-        const LongOut L = find_word_long(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, max_shift, P.lm, S.lwords,
-                                         S.tkeys, S.tmask, S.tcap_log2, epoch);
-        epoch = L.epoch;
+        LongOut L;
+        L.found = -1;
+        L.M = P.lm;
+        if (P.llds && S.ltab_log2 > 0 && 2u * (uint32_t)min(max(P.lm, LW_STEP), max_shift) <= (1u << S.ltab_log2)) {
+            // the first prefixes in the LDS word table
+            L = find_word_long<LdsU64>(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, max_shift, P.lm, S.lwords,
+                                       (LdsU64*)S.lkeys, (LdsU64*)S.lmask, S.ltab_log2, lepoch);
+            lepoch = L.epoch;
+        }
+        if (L.found == -1) {  // (the LDS table took none, or not the prefix L.M)
+            L = find_word_long<unsigned long long>(v.p, v.len, v.d, pos, w.lane, w.n, P.ac, max_shift, L.M, S.lwords,
+                                                   S.tkeys, S.tmask, S.tcap_log2, epoch);
+            epoch = L.epoch;
+        }
         n_shifts += L.shifts - head;
         if (L.found > 0) my_shift = L.my_shift;
         if (L.found >= 0) return L.found > 0;

@@ -27,8 +27,12 @@
 #include "common.hpp"
 #include "sa_device.hpp"
 
+// waves of k_align_jobs / k_align_sub per SIMD: 2 gives each wave 256
+// registers and no scratch spills (4: 128 registers, 648 bytes of scratch a
+// lane with the prefix search's call); C3 / C2 align -3 to -5 %, R3 and the
+// pair job level (gpurun_out r06c, profiles/r06c_ab_waves_per_eu.txt)
 #ifndef SA_WAVES_PER_EU
-#define SA_WAVES_PER_EU 4
+#define SA_WAVES_PER_EU 2
 #endif
 
 namespace npgx {
@@ -157,6 +161,13 @@ struct SaArgs {
     // copies, at twin_off[row] for the rows of jobs with a twin
     const char* twin_rows;
     const int64_t* twin_off;
+    // unsplit twins (order[] entries >= UTWIN_BASE, see "Unsplit twins" at
+    // align_device): per job the twin's output offset in utw_pool (-1: none),
+    // its state (0 running, 1 done, 2 overflowed) and its columns
+    const int64_t* utw_off;
+    int32_t* utw_state;
+    int32_t* utw_len;
+    unsigned char* utw_pool;
     int32_t cap_splits, cap_segs;
     int64_t cap_tgt, cap_find, cap_pool;
 };
@@ -1121,6 +1132,7 @@ static constexpr int SPLIT_RMAX = 1024;  // largest search half-width
 static constexpr int SPLIT_SPAN = 2 * SPLIT_RMAX + SPLIT_C + 1;  // word positions per row window
 static constexpr int SPLIT_CT = 256;     // LDS table of the candidate words
 static constexpr int SPLIT_KMAX = 1024;  // segments per job at most
+static constexpr int32_t UTWIN_BASE = 1 << 30;  // order[] entries >= this: the twin of unsplit job (entry - UTWIN_BASE)
 static constexpr int SPLIT_WAVES = 4;    // waves per sync state (rows dealt out)
 static constexpr int SPLIT_CH = ((SPLIT_SPAN + SPLIT_W + 63) / 64) * 64;  // window chars per wave
 static constexpr size_t SPLIT_LDS = (size_t)SPLIT_CT * 8 + (size_t)SPLIT_C * 4 +
@@ -2075,6 +2087,58 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
         jn = bcast(jn, 0);
         if (jn >= n_jobs) break;
         const int oj = a.order[jn];
+        if (oj >= UTWIN_BASE) {
+            // the twin of unsplit job tj: process_seqs of the job's rows
+            // reversed -- what fix_bad_regions re-aligns when the job's whole
+            // alignment is one bad region -- into its own output, beside the
+            // job's forward walk.  Twins come first in the queue, so every
+            // job that waits for its twin finds it running or done.
+            const int tj = oj - UTWIN_BASE;
+            const SaJob job = a.jobs[tj];
+            WaveCtx w;
+            w.lane = lane;
+            w.n = job.n;
+            w.rowmask = (job.n >= 64) ? ~0ull : ((1ull << job.n) - 1ull);
+            w.act = lane < job.n;
+            View v{nullptr, 0, 1};
+            if (w.act) {
+                v.p = a.rows + a.row_off[job.row0 + lane];
+                v.len = a.row_len[job.row0 + lane];
+            }
+            {  // the rows into LDS when they fit (as the job's own walk does)
+                int off = 0, tot = 0;
+                for (int r = 0; r < job.n; r++) {
+                    const int lr = bcast(v.len, r);
+                    if (lane == r) off = tot;
+                    tot += lr;
+                }
+                if (tot <= a.stage_bytes) {
+                    for (int r = 0; r < job.n; r++) {
+                        const char* src = bcast_ptr(v.p, r);
+                        const int lr = bcast(v.len, r), o = bcast(off, r);
+                        for (int q = lane; q < lr; q += 64) stage[o + q] = src[q];
+                    }
+                    __syncthreads();
+                    if (w.act) v.p = stage + off;
+                }
+            }
+            if (w.act) {  // char(q) = row[len - 1 - q]
+                v.p += v.len - 1;
+                v.d = -1;
+            }
+            ProcT<LONG> pr(w, a.P, S, (char*)(a.utw_pool + a.utw_off[tj]), job.cap, epoch, lepoch);
+            const int Lc = pr.run(v, 0);
+            const bool tovf = any_lane(w, pr.ovf);
+            epoch = pr.epoch;
+            lepoch = pr.lepoch;
+            __threadfence();  // the rows before the state
+            if (lane == 0) {
+                a.utw_len[tj] = Lc;
+                __hip_atomic_store(&a.utw_state[tj], tovf ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            continue;
+        }
         // oj < 0: segment task -oj-1 of a split job -- process_seqs of the row
         // suffixes from its sync state into its own output; the wave that
         // finishes the job's last segment goes on with the chained result in A
@@ -2247,7 +2311,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
                 t_regions = clock64() - t_reg0;
                 st_regions = R;
                 int colB = 0;
-                if (a.defer && L0 >= a.defer && n >= a.defer_rows && !(fast && R == 1 && bcast(rreg.z, 0)))
+                // the whole alignment one bad region and a twin walked the
+                // reversed rows: its result is the re-alignment
+                bool tw_ok = false;
+                if (a.utw_state && R == 1 && a.utw_off[j] >= 0) tw_ok = !(fast ? bcast(rreg.z, 0) : S.regions[0].z);
+                if (a.defer && L0 >= a.defer && n >= a.defer_rows && !(fast && R == 1 && bcast(rreg.z, 0)) && !tw_ok)
                     deferred = defer_regions(DeferOut{a.job_regions, a.job_nreg, a.subs, a.alloc, a.counters,
                                                       a.pool, a.pool_cap, a.max_sub, a.fin},
                                              n, j, job.reg_off, job.reg_cap, A, C, cap, R, fast, counted, rreg,
@@ -2290,6 +2358,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER
                     } else {
                         for (int c = rg.x + lane; c <= rg.y; c += 64) before += S.good_col[c];
                         before = wave_sum(before);
+                    }
+                    if (tw_ok) {  // (R == 1: the region is every column, colB = 0)
+                        int ts;
+                        while ((ts = __hip_atomic_load(&a.utw_state[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+                            __builtin_amdgcn_s_sleep(8);
+                        if (ts != 1) {  // the twin overflowed where this walk would have
+                            ovf = true;
+                            break;
+                        }
+                        const int Lc = __hip_atomic_load(&a.utw_len[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const char* tw = (const char*)(a.utw_pool + a.utw_off[j]);
+                        const int after = count_equal_cols(w, tw, cap, 0, Lc, nullptr);
+                        __syncthreads();
+                        if (after > before) {
+                            cm_copy_rev(w, tw, B, cap, colB, Lc);
+                            colB += Lc;
+                        } else {
+                            cm_copy(w, A, B, cap, rg.x, colB, len);
+                            colB += len;
+                        }
+                        __syncthreads();
+                        continue;
                     }
                     const View cv = stage_segment(w, A, cap, C, stage, sb, rg.x, rg.y + 1);
                     const int Lc = pr.run(cv, colB);
@@ -2536,6 +2626,7 @@ struct npgx_aligner {
     // only, the round-4 search)
     int long_head = 128;
     int long_m = 512;
+    int long_lds = 1;  // NPGX_LONG_LDS=0: the prefix search on the global word table only (A/B)
     // split jobs whose segment rooms for the whole row suffixes take at most
     // this many bytes get them (NPGX_SEG_FULL_MB; 0: the 8-sync-state rooms).
     // R3: the segment overflows (reason 202) go with them; the sub-job
@@ -2547,6 +2638,16 @@ struct npgx_aligner {
     // and their segments slow the launch -- 1 always, -1 in launches with few
     // tasks): see "Twins" at align_device
     int twins = 0;
+    // unsplit twins (see "Unsplit twins" at align_device): jobs of at least
+    // utw_rows rows (0: none; NPGX_UTWINS), while the launch stays within
+    // utw_max_tasks tasks (NPGX_UTWIN_TASKS)
+    int utw_rows = 3;
+    int utw_max_tasks = 256 * 4 * SA_WAVES_PER_EU;
+    std::vector<int64_t> h_utw_off;
+    std::vector<int32_t> h_utw_q;
+    DevBuf<unsigned char> d_utw_pool;
+    DevBuf<int64_t> d_utw_off;
+    DevBuf<int32_t> d_utw_st;
     std::vector<int64_t> h_twin_off;
     std::vector<int32_t> h_twin_list;
     DevBuf<char> d_twin;
@@ -2767,7 +2868,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     };
     put(al->d_row_off.p, ne_off.data(), ne_off.size() * 8);
     put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
-    Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf, al->long_head, al->long_m};
+    Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf, al->long_head, al->long_m, al->long_lds};
 
     std::vector<int32_t>& jlen = al->h_jlen;
     std::vector<int32_t>& jstat = al->h_jstat;
@@ -2975,6 +3076,34 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             for (int32_t j : todo)
                 if (!is_split[j]) queue.push_back(j);
         }
+        // Unsplit twins.  Most many-row alignments are one bad region as a
+        // whole (C3: 90 % of the 17-row flank jobs of the first iterations),
+        // and fix_bad_regions (SimilarAligner.cpp:428-459) then re-aligns the
+        // job's rows reversed after its forward walk: half of a launch's
+        // critical path.  Every unsplit job of at least utw_rows rows gets a
+        // twin task that walks its rows reversed in the same launch
+        // (k_align_jobs, ahead of the jobs in the queue); a job that finds
+        // itself one bad region takes the twin's result, any other leaves it
+        // unused.  The walk is the same process_seqs (bit-exact).  Twins are
+        // added while the launch stays within utw_max_tasks tasks.
+        int64_t utw_bytes = 0;
+        int n_utw = 0;
+        std::vector<int64_t>& uoff = al->h_utw_off;
+        if (attempt == 0 && o.aligner_type == 0 && al->utw_rows > 0) {
+            std::vector<int32_t>& tq = al->h_utw_q;
+            tq.clear();
+            uoff.assign((size_t)n_jobs, -1);
+            const int64_t room = (int64_t)al->utw_max_tasks - (int64_t)queue.size();
+            for (int32_t q : queue) {
+                if ((int64_t)tq.size() >= room) break;
+                if (q < 0 || jobs[q].n < al->utw_rows) continue;
+                uoff[(size_t)q] = utw_bytes;
+                utw_bytes += ((int64_t)jobs[q].n * jobs[q].cap + 255) & ~255ll;
+                tq.push_back(UTWIN_BASE + q);
+            }
+            n_utw = (int)tq.size();
+            if (n_utw) queue.insert(queue.begin(), tq.begin(), tq.end());
+        }
         const int nj = (int)queue.size();
         scr.grow((size_t)std::max<int64_t>(scratch, 256));  // (1.5x headroom: batches grow loop by loop)
         put(al->d_jobs.p, jobs.data(), jobs.size() * sizeof(SaJob));
@@ -2995,7 +3124,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         // (AnchorLoopFast at C4) then cost memory only where they run.
         int64_t cols_need = 256;  // good_col doubles as 64 ints of scratch
         for (int32_t q : queue)
-            if (q >= 0) cols_need = std::max<int64_t>(cols_need, (int64_t)jobs[q].cap + 1);
+            if (q >= 0 && q < UTWIN_BASE) cols_need = std::max<int64_t>(cols_need, (int64_t)jobs[q].cap + 1);
         uint32_t tlog = 10;
         while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
         int depth = max_len / std::max(1, o.aligned_check + 1) + 4;
@@ -3163,6 +3292,21 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         A.split_len = o.aligner_type == 0 ? al->split : 0;
         A.twin_rows = nullptr;
         A.twin_off = nullptr;
+        A.utw_off = nullptr;
+        A.utw_state = nullptr;
+        A.utw_len = nullptr;
+        A.utw_pool = nullptr;
+        if (n_utw) {
+            al->d_utw_pool.grow((size_t)std::max<int64_t>(utw_bytes, 256));
+            al->d_utw_off.grow((size_t)n_jobs);
+            al->d_utw_st.grow(2 * (size_t)n_jobs);
+            put(al->d_utw_off.p, uoff.data(), (size_t)n_jobs * 8);
+            zero(al->d_utw_st.p, 2 * (size_t)n_jobs * 4);
+            A.utw_off = al->d_utw_off.p;
+            A.utw_state = al->d_utw_st.p;
+            A.utw_len = al->d_utw_st.p + n_jobs;
+            A.utw_pool = al->d_utw_pool.p;
+        }
         A.post_area = nullptr;
         if (post_bytes > 0) {
             al->d_post.grow((size_t)post_bytes);
@@ -3525,6 +3669,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A1.split_len = 0;
             A1.twin_rows = nullptr;
             A1.twin_off = nullptr;
+            A1.utw_off = nullptr;
+            A1.utw_state = nullptr;
+            A1.utw_len = nullptr;
+            A1.utw_pool = nullptr;
             A1.cap_splits = A1.cap_segs = 0;
             A1.cap_tgt = A1.cap_find = A1.cap_pool = 0;
             size_t tr = al->timer.begin("align_jobs_retry", st, 0.0, 0);
@@ -3740,12 +3888,18 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         if (sp && *sp) a->split = std::max(0, atoi(sp));
         const char* lh = getenv("NPGX_LONG_HEAD");
         if (lh && *lh) a->long_head = std::max(0, atoi(lh));
+        const char* ll = getenv("NPGX_LONG_LDS");
+        if (ll && *ll) a->long_lds = atoi(ll) != 0;
         const char* lm = getenv("NPGX_LONG_M");
         if (lm && *lm) a->long_m = std::max(64, atoi(lm));
         const char* sf = getenv("NPGX_SEG_FULL_MB");
         if (sf && *sf) a->seg_full_bytes = (int64_t)std::max(0, atoi(sf)) << 20;
         const char* tw = getenv("NPGX_TWINS");
         if (tw && *tw) a->twins = atoi(tw) > 0 ? 1 : (atoi(tw) == 0 ? 0 : -1);
+        const char* ut = getenv("NPGX_UTWINS");
+        if (ut && *ut) a->utw_rows = std::max(0, atoi(ut));
+        const char* utt = getenv("NPGX_UTWIN_TASKS");
+        if (utt && *utt) a->utw_max_tasks = std::max(0, atoi(utt));
         const char* sb = getenv("NPGX_SLOT_BUDGET_MB");
         if (sb && *sb) {
             a->slot_budget = (int64_t)std::max(1, atoi(sb)) << 20;

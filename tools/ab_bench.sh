@@ -11,7 +11,7 @@ for i in $(seq 1 $N); do
     python - "$v" <<'PY'
 import json, sys
 d = json.loads(open("gpurun_out/ab_%s.log" % sys.argv[1]).read().strip().splitlines()[-1])
-s = d["last_step"]["ms_stage"]
+s = (d.get("stage_timeline") or {}).get("ms") or d["last_step"]["ms_stage_host"]
 al = d["last_step"].get("anchor_loop") or {}
 extra = ""
 if al:

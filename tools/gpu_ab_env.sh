@@ -18,7 +18,12 @@ for rep in 1 2; do
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 ls = d["last_step"]
-if "ms_stage" in ls:
+if d.get("stage_timeline"):
+    st = d["stage_timeline"]["ms"]
+    print("%-14s ms/step %.3f value %.1f align %.3f af %.3f ou %.3f fix_ends %.3f plan %.3f" % (
+        sys.argv[2], d["ms_per_step"], d["value"], st["align"], st["anchor_finder"], st["overlapless_union"],
+        st["fix_ends"], st["elf_plan"]))
+elif "ms_stage" in ls:
     st = ls["ms_stage"]
     print("%-14s ms/step %.3f value %.1f align %.3f (kernel wait %.3f) host %.3f" % (
         sys.argv[2], d["ms_per_step"], d["value"], st["align_batch"], st["align_kernel_wait"],

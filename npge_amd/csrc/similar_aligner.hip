@@ -1542,6 +1542,28 @@ __device__ __forceinline__ unsigned long long* split_bits(const SaArgs& a, const
     return sp.post >= 0 ? (unsigned long long*)(a.post_area + sp.post) : a.chain_bits + a.bits_off[s];
 }
 
+// rows 1..n-1 of four columns (a dword at src + r * scap each) handed to
+// put(r, x) after the loads of eight rows are in flight (a put's stores
+// cannot be proven apart from the next rows' loads, so load-store-load
+// would pay one memory round trip per row); returns the OR of every row's
+// XOR with row 0's dword x0 (zero bytes: identical columns)
+template <class Put>
+__device__ __forceinline__ uint32_t rows_dwords(const char* src, size_t scap, int n, uint32_t x0, Put put) {
+    uint32_t diff = 0;
+    for (int r0 = 1; r0 < n; r0 += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) x[u] = r0 + u < n ? *(const uint32_t*)(src + (size_t)(r0 + u) * scap) : x0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (r0 + u >= n) break;
+            diff |= x[u] ^ x0;
+            put(r0 + u, x[u]);
+        }
+    }
+    return diff;
+}
+
 // one workgroup per job split: the segment results in parallel into LDS, the
 // walk along the chain by one thread, the chain and its identical-column bit
 // words (cleared) to global memory
@@ -1619,17 +1641,14 @@ __global__ __launch_bounds__(POST_THREADS) void k_chain_copy(SaArgs a, int n_spl
         const int cs = (max(c0 - d0, 0)) & ~3, ce = min(c1 - d0, cols);
         for (int c = cs + 4 * tid; c < ce; c += 4 * POST_THREADS) {
             const uint32_t x0 = *(const uint32_t*)(src + c);  // (rows of 16-aligned length: in bounds)
-            uint32_t diff = 0;
             int lo_b = 0, hi_b = min(4, ce - c);  // this part's columns only
             if (d0 + c < c0) lo_b = c0 - (d0 + c);
             char* d = A + d0 + c;
-            for (int q = lo_b; q < hi_b; q++) d[q] = (char)(x0 >> (8 * q));
-            for (int r = 1; r < n; r++) {
-                const uint32_t x = *(const uint32_t*)(src + (size_t)r * g.cap + c);
-                diff |= x ^ x0;
+            const uint32_t diff = rows_dwords(src + c, (size_t)g.cap, n, x0, [&](int r, uint32_t x) {
                 char* dr = A + (size_t)r * cap + d0 + c;
                 for (int q = lo_b; q < hi_b; q++) dr[q] = (char)(x >> (8 * q));
-            }
+            });
+            for (int q = lo_b; q < hi_b; q++) d[q] = (char)(x0 >> (8 * q));
             unsigned long long m0 = 0, m1 = 0;
             const int col0 = d0 + c, w0 = col0 >> 6;
             for (int q = lo_b; q < hi_b; q++)
@@ -1956,14 +1975,11 @@ __global__ __launch_bounds__(POST_THREADS) void k_sub_post(SaArgs a, int first, 
             for (int c = 4 * tid; c < cols; c += 4 * POST_THREADS) {
                 const int nb = min(4, cols - c);
                 const uint32_t x0 = *(const uint32_t*)(src + c);
-                uint32_t diff = 0;
-                for (int b = 0; b < nb; b++) out[d0 + c + b] = (char)(x0 >> (8 * b));
-                for (int r = 1; r < n; r++) {
-                    const uint32_t x = *(const uint32_t*)(src + (size_t)r * g.cap + c);
-                    diff |= x ^ x0;
+                const uint32_t diff = rows_dwords(src + c, (size_t)g.cap, n, x0, [&](int r, uint32_t x) {
                     char* dr = out + (size_t)r * d.out_cap + d0 + c;
                     for (int b = 0; b < nb; b++) dr[b] = (char)(x >> (8 * b));
-                }
+                });
+                for (int b = 0; b < nb; b++) out[d0 + c + b] = (char)(x0 >> (8 * b));
                 for (int b = 0; b < nb; b++) same += !((diff >> (8 * b)) & 0xFFu);
             }
         }
@@ -2641,8 +2657,12 @@ struct npgx_aligner {
     // unsplit twins (see "Unsplit twins" at align_device): jobs of at least
     // utw_rows rows (0: none; NPGX_UTWINS), while the launch stays within
     // utw_max_tasks tasks (NPGX_UTWIN_TASKS)
+    // (C3 kernel traces, gpurun_out/r06e: with twins in a launch of 1020
+    // jobs its k_align_jobs went 363 -> 547 us -- twice the waves, half the
+    // LDS each -- while launches of 154-386 jobs gained up to a fifth: twins
+    // only while the launch keeps to about one wave per SIMD)
     int utw_rows = 3;
-    int utw_max_tasks = 256 * 4 * SA_WAVES_PER_EU;
+    int utw_max_tasks = 512;
     std::vector<int64_t> h_utw_off;
     std::vector<int32_t> h_utw_q;
     DevBuf<unsigned char> d_utw_pool;

@@ -51,13 +51,6 @@ static constexpr int WG = 256;         // windows per workgroup (4 waves)
 static constexpr int MAX_KB = 32;
 static constexpr int FKB = 4;          // hash functions with the batched-load path (fp 0.1 -> 3)
 
-struct SeqMeta {
-    int64_t size;
-    int64_t word_off;
-    int64_t n_off;
-    uint64_t order_off;   // sum of sizes of lower-ranked eligible sequences
-};
-
 struct Chunk {
     int32_t seq;
     int32_t pad;
@@ -628,6 +621,21 @@ struct npgx_af {
     StageTimer timer;
     std::vector<uint64_t> host_keys, host_H;
     std::vector<size_t> h_group_key;  // grouping: first key of each kept group
+    // Deferred host result (af_set_defer): the sorted FoundFragment keys of
+    // the last run stay on the device for a caller that builds its blocks
+    // there (DraftPangenome -> the device ExtendLoopFast); the host grouping
+    // (fragmenttg_postprocess, AnchorFinder.cpp:356-391) runs when a result,
+    // the used-hash set or the statistics are asked for, or before the next run
+    bool defer_host = false;
+    bool pending = false;       // the last run's keys are not grouped on the host yet
+    bool pending_used = false;  // ... nor their used hashes added (cleared by npgx_af_clear_used)
+    int64_t p_keep = 0;
+    uint64_t p_G = 0;
+    int p_key_bits = 0, p_k = 0;
+    int32_t p_R = 0;
+    std::vector<SeqMeta> p_meta;
+    std::vector<int32_t> p_by_rank;
+    DevBuf<int32_t> d_by_rank;   // rank -> input index (the device's key -> fragment conversion)
 
     void ensure_temp(size_t bytes) { temp.ensure(bytes); }
 };
@@ -705,6 +713,11 @@ static void comm_check(int rc, const char* what) {
     if (rc != 0) throw Error(NPGX_ERR_ARG, std::string("collective callback failed: ") + what);
 }
 
+static void af_group_host(npgx_af* af, const std::vector<uint64_t>& keys, const std::vector<uint64_t>& Hh,
+                          int key_bits, int32_t R, const SeqMeta* meta, const int32_t* by_rank, int k,
+                          bool add_used);
+static void af_materialize(npgx_af* af);
+
 static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     static const bool hdbg = getenv("NPGX_AF_DEBUG") != nullptr;  // host phase times to stderr
     const auto th0 = std::chrono::steady_clock::now();
@@ -714,6 +727,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     NPGX_HIP(hipSetDevice(af->device));
     hipStream_t st = af->stream;
     const int k = af->opt.anchor_size;
+    af_materialize(af);  // (the used set the last run added to)
     af->timer.reset();
     af->has_result = false;
     npgx_af_stats& S = af->stats;
@@ -1141,6 +1155,25 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
                                               0u, end_bit, st));
             af->timer.end(ti, st);
             const uint64_t keep = std::min<uint64_t>(C, (uint64_t)af->opt.max_anchor_fragments);
+            if (af->defer_host && !comm && keep > 0) {  // the keys stay on the device (af_device_keys)
+                af->pending = true;
+                af->pending_used = true;
+                af->p_keep = (int64_t)keep;
+                af->p_G = G;
+                af->p_key_bits = key_bits;
+                af->p_k = k;
+                af->p_R = R;
+                af->p_meta.assign(meta.begin(), meta.begin() + R);
+                af->p_by_rank.assign(ss->by_rank.begin(), ss->by_rank.begin() + R);
+                af->d_by_rank.ensure((size_t)std::max<int32_t>(R, 1));
+                int32_t* hb = (int32_t*)af->pinned_dl.ensure((size_t)R / 2 + 2);
+                memcpy(hb, af->p_by_rank.data(), (size_t)R * 4);
+                NPGX_HIP(hipMemcpyAsync(af->d_by_rank.p, hb, (size_t)R * 4, hipMemcpyHostToDevice, st));
+                NPGX_HIP(stream_wait(st));
+                S.n_blocks = S.n_fragments = -1;  // (af_materialize)
+                af->has_result = true;
+                return;
+            }
             keys.resize(keep);
             Hh.resize(G);
             af->pinned_dl.ensure((keep + G) * 8);
@@ -1154,7 +1187,19 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     }
 
     h_dl = hms();
-    // --- fragmenttg_postprocess (AnchorFinder.cpp:356-391) on the truncated list
+    af_group_host(af, keys, Hh, key_bits, R, meta.data(), ss->by_rank.data(), k, true);
+    if (hdbg)
+        fprintf(stderr, "af host: prep %.3f ms, results downloaded at %.3f ms, grouping %.3f ms (%zu keys, %lld blocks)\n",
+                h_prep, h_dl, hms() - h_dl, keys.size(), (long long)S.n_blocks);
+}
+
+// fragmenttg_postprocess (AnchorFinder.cpp:356-391) on the truncated key list
+// (keys sorted, H the kept hashes): the groups, the used-hash quirk (add_used)
+// and the host result
+static void af_group_host(npgx_af* af, const std::vector<uint64_t>& keys, const std::vector<uint64_t>& Hh,
+                          int key_bits, int32_t R, const SeqMeta* meta, const int32_t* by_rank, int k,
+                          bool add_used) {
+    npgx_af_stats& S = af->stats;
     std::vector<uint64_t> prefix2(R);
     for (int32_t r = 0; r < R; r++) prefix2[r] = 2ull * meta[r].order_off;
     const uint64_t key_mask = key_bits >= 64 ? ~0ull : ((1ull << key_bits) - 1);
@@ -1171,7 +1216,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         const uint64_t idx = keys[i] >> key_bits;
         size_t j = i + 1;
         while (j < nk && (keys[j] >> key_bits) == idx) j++;
-        if (!first_group) af->used.push_back(Hh[idx]);  // quirk: not the first group
+        if (!first_group && add_used) af->used.push_back(Hh[idx]);  // quirk: not the first group
         first_group = false;
         if (j - i >= 2) {
             af->r_block_start.push_back(nout);
@@ -1187,7 +1232,6 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     af->r_ori.resize((size_t)nout);
     // pass 2: the fragments (FoundFragment::make_fragment :240-246), groups on
     // host threads; a group's keys ascend, so its sequence rank only moves forward
-    const double h_pass1 = hms();
     const size_t ng = gk.size(), per = 256;  // groups per task: few tasks on the pool's shared counter
     heavy_for((ng + per - 1) / per, nout * 16, [&](size_t t) {
       for (size_t g = t * per; g < std::min(ng, (t + 1) * per); g++) {
@@ -1201,7 +1245,7 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
             const uint64_t size = (uint64_t)meta[(size_t)r].size;
             const bool direct = pos2 < size;
             const int64_t mn = (int64_t)(direct ? pos2 : pos2 - size);
-            af->r_seq[(size_t)o] = ss->by_rank[(size_t)r];
+            af->r_seq[(size_t)o] = by_rank[(size_t)r];
             af->r_min[(size_t)o] = mn;
             af->r_max[(size_t)o] = mn + k - 1;
             af->r_ori[(size_t)o] = direct ? 1 : -1;
@@ -1214,9 +1258,41 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
     S.n_fragments = (int64_t)af->r_seq.size();
     S.n_used = (int64_t)af->used.size();
     af->has_result = true;
-    if (hdbg)
-        fprintf(stderr, "af host: prep %.3f ms, results downloaded at %.3f ms, grouping %.3f ms (groups %.3f ms; "
-                "%zu keys, %lld blocks)\n", h_prep, h_dl, hms() - h_dl, h_pass1 - h_dl, keys.size(), (long long)S.n_blocks);
+}
+
+// the deferred host result of the last run (see npgx_af.defer_host)
+static void af_materialize(npgx_af* af) {
+    if (!af->pending) return;
+    af->pending = false;
+    hipStream_t st = af->stream;
+    NPGX_HIP(hipSetDevice(af->device));
+    std::vector<uint64_t>& keys = af->host_keys;
+    std::vector<uint64_t>& Hh = af->host_H;
+    keys.resize((size_t)af->p_keep);
+    Hh.resize((size_t)af->p_G);
+    af->pinned_dl.ensure((size_t)(af->p_keep + af->p_G) * 8 + 8);
+    uint64_t* pk = af->pinned_dl.p;
+    if (af->p_keep) NPGX_HIP(hipMemcpyAsync(pk, af->cand_sorted.p, (size_t)af->p_keep * 8, hipMemcpyDeviceToHost, st));
+    if (af->p_G) NPGX_HIP(hipMemcpyAsync(pk + af->p_keep, af->huniq.p, (size_t)af->p_G * 8, hipMemcpyDeviceToHost, st));
+    NPGX_HIP(stream_wait(st));
+    memcpy(keys.data(), pk, (size_t)af->p_keep * 8);
+    memcpy(Hh.data(), pk + af->p_keep, (size_t)af->p_G * 8);
+    af_group_host(af, keys, Hh, af->p_key_bits, af->p_R, af->p_meta.data(), af->p_by_rank.data(), af->p_k,
+                  af->pending_used);
+}
+
+void af_set_defer(npgx_af* af, bool on) { af->defer_host = on; }
+
+bool af_device_keys(npgx_af* af, AfDevKeys* o) {
+    if (!af->pending) return false;
+    o->keys = af->cand_sorted.p;
+    o->keep = af->p_keep;
+    o->key_bits = af->p_key_bits;
+    o->k = af->p_k;
+    o->R = af->p_R;
+    o->meta = af->d_meta.p;
+    o->by_rank = af->d_by_rank.p;
+    return true;
 }
 
 }  // namespace npgx
@@ -1282,6 +1358,7 @@ int npgx_af_run_sharded(npgx_af* af, const npgx_seqset* s, const npgx_comm* comm
 int npgx_af_stats_get(const npgx_af* af, npgx_af_stats* out) {
     return guard([&] {
         NPGX_REQUIRE(af && out, NPGX_ERR_ARG, "null argument");
+        af_materialize(const_cast<npgx_af*>(af));
         *out = af->stats;
     });
 }
@@ -1290,6 +1367,7 @@ int npgx_af_result_counts(const npgx_af* af, int64_t* nb, int64_t* nf) {
     return guard([&] {
         NPGX_REQUIRE(af && nb && nf, NPGX_ERR_ARG, "null argument");
         NPGX_REQUIRE(af->has_result, NPGX_ERR_STATE, "no AnchorFinder result yet");
+        af_materialize(const_cast<npgx_af*>(af));
         *nb = (int64_t)af->r_block_start.size() - 1;
         *nf = (int64_t)af->r_seq.size();
     });
@@ -1300,6 +1378,7 @@ int npgx_af_result_copy(const npgx_af* af, int64_t* block_start, int32_t* seq, i
     return guard([&] {
         NPGX_REQUIRE(af, NPGX_ERR_ARG, "null argument");
         NPGX_REQUIRE(af->has_result, NPGX_ERR_STATE, "no AnchorFinder result yet");
+        af_materialize(const_cast<npgx_af*>(af));
         const size_t nf = af->r_seq.size();
         if (block_start) memcpy(block_start, af->r_block_start.data(), af->r_block_start.size() * 8);
         if (seq) memcpy(seq, af->r_seq.data(), nf * 4);
@@ -1312,6 +1391,7 @@ int npgx_af_result_copy(const npgx_af* af, int64_t* block_start, int32_t* seq, i
 int npgx_af_used_hashes(const npgx_af* af, uint64_t* out, int64_t cap, int64_t* n) {
     return guard([&] {
         NPGX_REQUIRE(af && n, NPGX_ERR_ARG, "null argument");
+        af_materialize(const_cast<npgx_af*>(af));
         *n = (int64_t)af->used.size();
         if (out) memcpy(out, af->used.data(), (size_t)std::min<int64_t>(cap, *n) * 8);
     });
@@ -1321,6 +1401,7 @@ int npgx_af_clear_used(npgx_af* af) {
     return guard([&] {
         NPGX_REQUIRE(af, NPGX_ERR_ARG, "null argument");
         af->used.clear();
+        af->pending_used = false;  // (a deferred result's used hashes go with the rest)
         af->used_dirty = true;
     });
 }

@@ -352,10 +352,40 @@ struct JobRows {
 // (device, one JobRows per job); `err` (device) is set when a job overflows
 // both attempts.  No job may have more than 64 non-empty rows (k_align_wide
 // is host-driven); AlignResult is left empty.
+// a sequence of an AnchorFinder run, by rank (anchor_finder.hip)
+struct SeqMeta {
+    int64_t size;
+    int64_t word_off;
+    int64_t n_off;
+    uint64_t order_off;   // sum of sizes of lower-ranked eligible sequences
+};
+
+// The last AnchorFinder run's sorted FoundFragment keys on the device, when
+// the run deferred its host result (af_set_defer): key = group index <<
+// key_bits | 2 * order_off(rank) + position (the reverse strand's positions
+// after the direct ones), the first `keep` keys kept (max-anchor-fragments)
+struct AfDevKeys {
+    const uint64_t* keys;
+    int64_t keep;
+    int key_bits, k;
+    int32_t R;              // eligible sequences (the ranks with meta)
+    const SeqMeta* meta;    // by rank
+    const int32_t* by_rank; // rank -> input index
+};
+void af_set_defer(npgx_af* af, bool on);
+bool af_device_keys(npgx_af* af, AfDevKeys* out);  // false: no deferred result pending
+
 struct AlignAsync {
     JobRows* out;
     int32_t* err;
     uint32_t* epoch;  // (device) the launches' highest word-table epoch; hand it back with aligner_note_epoch
+    // optional, uniform jobs (the device ExtendLoopFast's flank batches):
+    // job j is ujobs[j].x rows of ujobs[j].y > 0 letters each, its rows
+    // consecutive in the device arrays d_row_off / d_row_len (the caller's
+    // plan wrote them); the host row arrays of align_device are then unused
+    const int2* ujobs = nullptr;
+    const int64_t* d_row_off = nullptr;
+    const int32_t* d_row_len = nullptr;
 };
 // the highest word-table epoch an async call reached (read from AlignAsync::epoch
 // after the caller's wait): the next call's tables start above it

@@ -2734,8 +2734,9 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     hipStream_t st = al->stream;
     const npgx_align_options& o = al->opt;
     NPGX_REQUIRE(n_jobs >= 0, NPGX_ERR_ARG, "n_jobs < 0");
-    const int64_t r_base = n_jobs ? job_row_start[0] : 0;
-    const int64_t n_rows = n_jobs ? (int64_t)job_row_start[n_jobs] - r_base : 0;
+    const int2* uj = as ? as->ujobs : nullptr;  // uniform jobs: no host row arrays
+    const int64_t r_base = (n_jobs && !uj) ? job_row_start[0] : 0;
+    const int64_t n_rows = (n_jobs && !uj) ? (int64_t)job_row_start[n_jobs] - r_base : 0;
     // host arrays kept in the handle across calls (capacity reused)
     std::vector<SaJob>& jobs = al->h_jobs;
     std::vector<int64_t>& ne_off = al->h_ne_off;
@@ -2743,7 +2744,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     jobs.resize(n_jobs);
     ne_off.clear();
     ne_len.clear();
-    res.row_ne.assign((size_t)std::max<int64_t>(n_rows, 1), -1);
+    if (!uj) res.row_ne.assign((size_t)std::max<int64_t>(n_rows, 1), -1);
+    int64_t u_rows = 0;  // (uniform jobs: rows so far)
     std::vector<double>& cost = al->h_cost;
     cost.resize(n_jobs);
     std::vector<int32_t>& jsum = al->h_jsum;  // residues per job
@@ -2759,13 +2761,22 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
     // at least this many columns wide
     const int min_width = std::max(1, std::min(o.min_length, (o.min_length + wf - 1) / std::max(wf, 1)));
     for (int32_t j = 0; j < n_jobs; j++) {
-        const int64_t r0 = job_row_start[j], r1 = job_row_start[j + 1];
-        NPGX_REQUIRE(r1 >= r0, NPGX_ERR_ARG, "job_row_start not monotone");
         SaJob& J = jobs[j];
-        J.row0 = (int64_t)ne_len.size();
         int n = 0;
         int64_t sum = 0;
         int mx = 0;
+        if (uj) {
+            const int2 q = uj[j];
+            NPGX_REQUIRE(q.x >= 0 && q.x <= 64 && q.y > 0 && q.y < (1 << 30), NPGX_ERR_RANGE, "uniform job out of range");
+            J.row0 = u_rows;
+            u_rows += q.x;
+            n = q.x;
+            sum = (int64_t)q.x * q.y;
+            mx = q.x ? q.y : 0;
+        }
+        const int64_t r0 = uj ? 0 : job_row_start[j], r1 = uj ? 0 : job_row_start[j + 1];
+        NPGX_REQUIRE(r1 >= r0, NPGX_ERR_ARG, "job_row_start not monotone");
+        if (!uj) J.row0 = (int64_t)ne_len.size();
         for (int64_t r = r0; r < r1; r++) {
             const int64_t len = row_len[r];
             NPGX_REQUIRE(len >= 0 && len < (1ll << 30), NPGX_ERR_RANGE, "row length out of range");
@@ -2886,8 +2897,14 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->h_ops.clear();
         al->h_blob.clear();
     };
-    put(al->d_row_off.p, ne_off.data(), ne_off.size() * 8);
-    put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
+    if (!uj) {
+        put(al->d_row_off.p, ne_off.data(), ne_off.size() * 8);
+        put(al->d_row_len.p, ne_len.data(), ne_len.size() * 4);
+    }
+    const int64_t* const d_roff = uj ? as->d_row_off : al->d_row_off.p;
+    const int32_t* const d_rlen = uj ? as->d_row_len : al->d_row_len.p;
+    // row i of job j's letters (host)
+    auto row_len_at = [&](int32_t j, int i) -> int32_t { return uj ? uj[j].y : ne_len[jobs[j].row0 + i]; };
     Params P{o.mismatch_check, o.gap_check, o.aligned_check, o.min_length, wf, al->long_head, al->long_m, al->long_lds};
 
     std::vector<int32_t>& jlen = al->h_jlen;
@@ -2917,7 +2934,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         for (int32_t j : order) {
             SaJob& J = j1[j];
             int64_t sum = 0;
-            for (int i = 0; i < J.n; i++) sum += ne_len[J.row0 + i];
+            for (int i = 0; i < J.n; i++) sum += row_len_at(j, i);
             J.cap = (int32_t)((std::max<int64_t>(sum, 1) + 15) & ~15ll);
             J.scratch = scratch1;
             scratch1 += (3ll * J.n * J.cap + 255) & ~255ll;
@@ -2959,7 +2976,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 max_n = std::max(max_n, J.n);
                 max_len = std::max(max_len, jmax[j]);
                 int64_t sum = 0;
-                for (int i = 0; i < J.n; i++) sum += ne_len[J.row0 + i];
+                for (int i = 0; i < J.n; i++) sum += row_len_at(j, i);
                 J.cap = (int32_t)((std::max<int64_t>(sum, 1) + 15) & ~15ll);
                 J.scratch = scratch;
                 scratch += (3ll * J.n * J.cap + 255) & ~255ll;
@@ -3051,7 +3068,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         }
         int64_t twin_bytes = 0;
         if (twins) {
-            al->h_twin_off.assign(ne_len.size(), 0);
+            al->h_twin_off.assign(uj ? (size_t)u_rows : ne_len.size(), 0);
             al->h_twin_list.clear();
             for (int si = 0; si < n_js; si++) {
                 SaSplit tw = splits[si];
@@ -3059,7 +3076,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 for (int i = 0; i < J.n; i++) {
                     al->h_twin_off[J.row0 + i] = twin_bytes;
                     al->h_twin_list.push_back((int32_t)(J.row0 + i));
-                    twin_bytes += ne_len[J.row0 + i];
+                    twin_bytes += row_len_at(tw.job, i);
                 }
                 const int ti = (int)splits.size();
                 tw.sub = -2;
@@ -3186,8 +3203,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         pmark(4);
         SaArgs A;
         A.rows = d_rows;
-        A.row_off = al->d_row_off.p;
-        A.row_len = al->d_row_len.p;
+        A.row_off = d_roff;
+        A.row_len = d_rlen;
         A.jobs = al->d_jobs.p;
         A.order = al->d_order.p;
         A.n_jobs = nj;
@@ -3408,7 +3425,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             flush();
             if (twins) {
                 hipLaunchKernelGGL(k_twin_rows, dim3((unsigned)std::min<size_t>(al->h_twin_list.size(), 4096)),
-                                   dim3(256), 0, st, d_rows, al->d_row_off.p, al->d_row_len.p, al->d_twin_list.p,
+                                   dim3(256), 0, st, d_rows, d_roff, d_rlen, al->d_twin_list.p,
                                    (int)al->h_twin_list.size(), al->d_twin_off.p, al->d_twin.p);
                 NPGX_HIP(hipGetLastError());
             }

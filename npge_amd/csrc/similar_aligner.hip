@@ -1133,7 +1133,10 @@ static constexpr int SPLIT_SPAN = 2 * SPLIT_RMAX + SPLIT_C + 1;  // word positio
 static constexpr int SPLIT_CT = 256;     // LDS table of the candidate words
 static constexpr int SPLIT_KMAX = 1024;  // segments per job at most
 static constexpr int32_t UTWIN_BASE = 1 << 30;  // order[] entries >= this: the twin of unsplit job (entry - UTWIN_BASE)
-static constexpr int SPLIT_WAVES = 4;    // waves per sync state (rows dealt out)
+#ifndef SA_SPLIT_WAVES
+#define SA_SPLIT_WAVES 4
+#endif
+static constexpr int SPLIT_WAVES = SA_SPLIT_WAVES;  // waves per sync state (rows dealt out)
 static constexpr int SPLIT_CH = ((SPLIT_SPAN + SPLIT_W + 63) / 64) * 64;  // window chars per wave
 static constexpr size_t SPLIT_LDS = (size_t)SPLIT_CT * 8 + (size_t)SPLIT_C * 4 +
                                     (size_t)SPLIT_WAVES * SPLIT_C * 8 + (size_t)64 * SPLIT_C * 2 +

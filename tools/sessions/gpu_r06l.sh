@@ -17,4 +17,12 @@ for cfg in C3 R3; do
   step "utwin tasks $cfg"
   timeout -k 10 600 tools/gpu_ab_env.sh r06l NPGX_UTWIN_TASKS 512 768 --config $cfg --steps 10 --warmup 3 || exit 1
 done
+step "split waves 8: parity"
+NPGX_LIB=libnpge_amd_sw8.so timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_similar_aligner_gpu.py tests/test_fullsize_gpu.py > $O/pytest_sw8.log 2>&1 || { tail -30 $O/pytest_sw8.log; exit 1; }
+tail -1 $O/pytest_sw8.log
+for cfg in C3 R3; do
+  step "split waves 8: ab $cfg"
+  timeout -k 10 600 tools/ab_bench.sh libnpge_amd_sw8.so 2 --config $cfg --no-pairs-line > $O/ab_sw8_$cfg.txt 2>&1 || { tail -5 $O/ab_sw8_$cfg.txt; exit 1; }
+  cut -c1-150 $O/ab_sw8_$cfg.txt
+done
 step done

@@ -1134,7 +1134,7 @@ static constexpr int SPLIT_CT = 256;     // LDS table of the candidate words
 static constexpr int SPLIT_KMAX = 1024;  // segments per job at most
 static constexpr int32_t UTWIN_BASE = 1 << 30;  // order[] entries >= this: the twin of unsplit job (entry - UTWIN_BASE)
 #ifndef SA_SPLIT_WAVES
-#define SA_SPLIT_WAVES 4
+#define SA_SPLIT_WAVES 8  // (4 -> 8: C3 align -0.2 ms, R3 -0.2 ms; profiles/r06l_aligner_param_sweep.txt)
 #endif
 static constexpr int SPLIT_WAVES = SA_SPLIT_WAVES;  // waves per sync state (rows dealt out)
 static constexpr int SPLIT_CH = ((SPLIT_SPAN + SPLIT_W + 63) / 64) * 64;  // window chars per wave
@@ -3133,7 +3133,11 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             std::vector<int32_t>& tq = al->h_utw_q;
             tq.clear();
             uoff.assign((size_t)n_jobs, -1);
-            const int64_t room = (int64_t)al->utw_max_tasks - (int64_t)queue.size();
+            // up to utw_max_tasks tasks, and in any launch the heaviest jobs'
+            // twins that fill the last 256-task step: the LDS share of every
+            // workgroup (one per 256 tasks and CU) stays what it was
+            const int64_t q = (int64_t)queue.size();
+            const int64_t room = std::max<int64_t>((int64_t)al->utw_max_tasks - q, (q + 255) / 256 * 256 - q);
             for (int32_t q : queue) {
                 if ((int64_t)tq.size() >= room) break;
                 if (q < 0 || jobs[q].n < al->utw_rows) continue;

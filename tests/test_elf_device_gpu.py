@@ -39,22 +39,28 @@ def test_ou_device_many_blocks(max_len, self_overlap):
     assert 0 < len(want) <= len(blocks)
 
 
-def test_ou_device_ties_and_chains():
+@pytest.mark.parametrize("n_chain,n_dup", [(2000, 300), (1700, 300), (1, 0), (0, 2)])
+def test_ou_device_ties_and_chains(n_chain, n_dup):
     """Blocks of equal size and length (the minimum fragment, then the sorted
     fragment list, then the input order decide) in long overlap chains (the
     priority sweeps run many rounds), and blocks without fragments in range
-    of nothing else."""
+    of nothing else; down to one block of two fragments (its fragments
+    sorted all the same: with one block the block sort is skipped) and two
+    equal blocks."""
     rng = np.random.default_rng(5)
     n_seqs, seq_len = 3, 200000
     seqs = ["".join(rng.choice(list("ACGT"), size=seq_len)) for _ in range(n_seqs)]
     names = ["t%d&c&c" % i for i in range(n_seqs)]
     blocks = []
-    for i in range(2000):  # a chain along sequence 0: each block overlaps the next
+    for i in range(n_chain):  # a chain along sequence 0: each block overlaps the next
         a = 50 * i
         blocks.append([(0, a, a + 60, 1, None), (1 + i % 2, a, a + 60, -1 if i % 3 else 1, None)])
-    for i in range(300):  # duplicates of earlier blocks' first fragments
-        j = int(rng.integers(0, 2000))
-        blocks.append([blocks[j][0], (2, 150000 + 70 * i, 150000 + 70 * i + 60, 1, None)])
+    for i in range(n_dup):  # duplicates of earlier blocks' first fragments
+        if n_chain:
+            j = int(rng.integers(0, n_chain))
+            blocks.append([blocks[j][0], (2, 150000 + 70 * i, 150000 + 70 * i + 60, 1, None)])
+        else:  # two equal blocks
+            blocks.append([(0, 100, 160, 1, None), (1, 500, 560, -1, None)])
     perm = rng.permutation(len(blocks))
     blocks = [blocks[int(k)] for k in perm]
     ss, eng = _engine(seqs, names)

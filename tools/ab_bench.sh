@@ -11,7 +11,8 @@ for i in $(seq 1 $N); do
     python - "$v" <<'PY'
 import json, sys
 d = json.loads(open("gpurun_out/ab_%s.log" % sys.argv[1]).read().strip().splitlines()[-1])
-s = (d.get("stage_timeline") or {}).get("ms") or d["last_step"]["ms_stage_host"]
+ls = d["last_step"]
+s = (d.get("stage_timeline") or {}).get("ms") or ls.get("ms_stage_host") or ls.get("mean_pair_ms") or {}
 al = d["last_step"].get("anchor_loop") or {}
 extra = ""
 if al:

@@ -27,13 +27,20 @@
 #include "common.hpp"
 #include "sa_device.hpp"
 
-// waves of k_align_jobs / k_align_sub per SIMD: 2 gives each wave 256
-// registers and no scratch spills (4: 128 registers, 648 bytes of scratch a
-// lane with the prefix search's call); C3 / C2 align -3 to -5 %, R3 and the
-// pair job level (gpurun_out r06c, profiles/r06c_ab_waves_per_eu.txt)
+// waves of k_align_jobs / k_align_sub per SIMD, chosen per launch: 2 gives
+// each wave 256 registers and no scratch spills (4: 128 registers, 648 bytes
+// of scratch a lane with the prefix search's call) -- C3 / C2 align -3 to -5
+// %, R3 and the pair job level (profiles/r06c_ab_waves_per_eu.txt); a launch
+// with more tasks than 2 waves a SIMD hold (SA_WAVES_MANY_AT) takes the
+// 4-wave form: C5's first launches (tens of thousands of 8-row jobs) ran
+// 30 ms a step slower with 2 (profiles/r06t_c5_waves_twins_anchor_ab.txt)
 #ifndef SA_WAVES_PER_EU
 #define SA_WAVES_PER_EU 2
 #endif
+#ifndef SA_WAVES_MANY
+#define SA_WAVES_MANY 4
+#endif
+static constexpr int SA_WAVES_MANY_AT = 256 * 4 * SA_WAVES_PER_EU;
 
 namespace npgx {
 
@@ -906,8 +913,8 @@ __device__ __forceinline__ int fin_width(const SaArgs& a, int4 rg) {
 // k_align_sub: every bad region of every deferred job, one wave each; with a
 // plan (k_plan_subs) the segments of the split sub-jobs first, then the other
 // sub-jobs
-template <bool LONG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER_EU))) void k_align_sub(SaArgs a) {
+template <bool LONG, int W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_align_sub(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
     SlotEnv e = slot_env(a, lds_u64);
@@ -2087,8 +2094,8 @@ __global__ __launch_bounds__(POST_THREADS) void k_fin_copy(SaArgs a, int lds_int
     }
 }
 
-template <bool LONG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SA_WAVES_PER_EU))) void k_align_jobs(SaArgs a) {
+template <bool LONG, int W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(W))) void k_align_jobs(SaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_u64[];
     const int lane = threadIdx.x;
     SlotEnv e = slot_env(a, lds_u64);
@@ -2884,6 +2891,14 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         al->h_ops.push_back(ScatterOp{d, (int64_t)at, (int64_t)bytes});
     };
     auto zero = [&](void* d, size_t bytes) { al->h_ops.push_back(ScatterOp{d, -1, (int64_t)bytes}); };
+    // k_align_jobs / k_align_sub in the form of the set (long head or not) and
+    // of the launch's waves a SIMD
+    typedef void (*SaKernel)(SaArgs);
+    auto launch_sa = [&](SaKernel lf, SaKernel sf, SaKernel lm, SaKernel sm, int wv, size_t g, size_t lds,
+                         const SaArgs& X) {
+        const bool lh = al->long_head > 0, many = wv == SA_WAVES_MANY;
+        hipLaunchKernelGGL(lh ? (many ? lm : lf) : (many ? sm : sf), dim3((unsigned)g), dim3(64), lds, st, X);
+    };
     auto flush = [&]() {
         if (al->h_ops.empty()) return;
         const size_t nop = al->h_ops.size(), head = (nop * sizeof(ScatterOp) + 15) & ~(size_t)15;
@@ -3157,7 +3172,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         pmark(3);
         // per-slot scratch: the word table (20 B an entry), the append_aligned
         // stack (1028 B a level) and the regions of unsplit jobs (17 B a
-        // column), for SA_WAVES_PER_EU waves on each of the 4 SIMDs of the 256
+        // column), for wv waves on each of the 4 SIMDs of the 256
         // CUs.  The largest job's bounds set the sizes (a call inserts at most
         // rows x (length + 1) words and nests at most length / (aligned_check
         // + 1) deep).  When that many slots at those sizes pass the budget,
@@ -3173,7 +3188,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
         int depth = max_len / std::max(1, o.aligned_check + 1) + 4;
         auto per_slot = [&](uint32_t tl, int dp) { return (20ll << tl) + 1028ll * dp + 17ll * cols_need; };
-        size_t slots = (size_t)std::max(1, std::min(nj, 256 * 4 * SA_WAVES_PER_EU));
+        const int wv = nj > SA_WAVES_MANY_AT ? SA_WAVES_MANY : SA_WAVES_PER_EU;  // this launch's waves a SIMD
+        size_t slots = (size_t)std::max(1, std::min(nj, 256 * 4 * wv));
         const int64_t mem_budget = std::max<int64_t>(al->slot_budget, 1ll << 22);
         if (attempt == 0)
             while ((int64_t)slots * per_slot(tlog, depth) > mem_budget && (tlog > 16 || depth > 512)) {
@@ -3293,8 +3309,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         int64_t max_rows = 0;
         for (int32_t j : todo) max_rows = std::max<int64_t>(max_rows, jsum[j]);
         static const int64_t per_cu_max = getenv("NPGX_SA_PER_CU_MAX") ? std::max(1, atoi(getenv("NPGX_SA_PER_CU_MAX")))
-                                                                       : 4 * SA_WAVES_PER_EU;  // (A/B: LDS per slot)
-        const int64_t per_cu = std::min<int64_t>(std::min<int64_t>(4 * SA_WAVES_PER_EU, per_cu_max),
+                                                                       : 4 * SA_WAVES_MANY;  // (A/B: LDS per slot)
+        const int64_t per_cu = std::min<int64_t>(std::min<int64_t>(4 * wv, per_cu_max),
                                                  std::max<int64_t>(1, ((int64_t)nj + 255) / 256));
         const int64_t budget = LDS_PER_CU / per_cu;
         // word history of the row-parallel search (HIST_SHIFTS x 64 words) when
@@ -3454,8 +3470,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         flush();
         size_t ti = al->timer.begin(attempt == 0 ? "align_jobs" : "align_jobs_retry", st,
                                     double(residues) * 2.0, residues);
-        if (al->long_head > 0) hipLaunchKernelGGL(k_align_jobs<true>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
-        else hipLaunchKernelGGL(k_align_jobs<false>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+        launch_sa(k_align_jobs<true, SA_WAVES_PER_EU>, k_align_jobs<false, SA_WAVES_PER_EU>,
+                  k_align_jobs<true, SA_WAVES_MANY>, k_align_jobs<false, SA_WAVES_MANY>, wv, slots, lds_bytes, A);
         NPGX_HIP(hipGetLastError());
         al->timer.end(ti, st);
         pmark(7);
@@ -3511,8 +3527,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 al->timer.end(ti, st);
             }
             ti = al->timer.begin("align_sub", st, 0.0, 0);
-            if (al->long_head > 0) hipLaunchKernelGGL(k_align_sub<true>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
-            else hipLaunchKernelGGL(k_align_sub<false>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A);
+            launch_sa(k_align_sub<true, SA_WAVES_PER_EU>, k_align_sub<false, SA_WAVES_PER_EU>,
+                      k_align_sub<true, SA_WAVES_MANY>, k_align_sub<false, SA_WAVES_MANY>, wv, slots, lds_bytes, A);
             NPGX_HIP(hipGetLastError());
             al->timer.end(ti, st);
             if (split_subs) {  // the split sub-jobs' chains
@@ -3529,8 +3545,8 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
                 A2.rq = al->d_rq.p;
                 ti = al->timer.begin("align_sub_retry", st, 0.0, 0);
                 hipLaunchKernelGGL(k_sub_retry_list, dim3(256), dim3(256), 0, st, A2);
-                if (al->long_head > 0) hipLaunchKernelGGL(k_align_sub<true>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A2);
-                else hipLaunchKernelGGL(k_align_sub<false>, dim3((unsigned)slots), dim3(64), lds_bytes, st, A2);
+                launch_sa(k_align_sub<true, SA_WAVES_PER_EU>, k_align_sub<false, SA_WAVES_PER_EU>,
+                          k_align_sub<true, SA_WAVES_MANY>, k_align_sub<false, SA_WAVES_MANY>, wv, slots, lds_bytes, A2);
                 NPGX_HIP(hipGetLastError());
                 al->timer.end(ti, st);
             }
@@ -3720,8 +3736,10 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
             A1.cap_splits = A1.cap_segs = 0;
             A1.cap_tgt = A1.cap_find = A1.cap_pool = 0;
             size_t tr = al->timer.begin("align_jobs_retry", st, 0.0, 0);
-            if (al->long_head > 0) hipLaunchKernelGGL(k_align_jobs<true>, dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
-            else hipLaunchKernelGGL(k_align_jobs<false>, dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
+            if (al->long_head > 0)
+                hipLaunchKernelGGL((k_align_jobs<true, SA_WAVES_PER_EU>), dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
+            else
+                hipLaunchKernelGGL((k_align_jobs<false, SA_WAVES_PER_EU>), dim3((unsigned)slots1), dim3(64), lds_bytes, st, A1);
             al->timer.end(tr, st);
             hipLaunchKernelGGL(k_job_rows, dim3(jg), dim3(256), 0, st, al->d_jobs.p, al->d_jobs1.p, al->d_retried.p,
                                d_job_status, d_job_len, n_jobs, scr.p, al->d_scratch2.p, as->out, as->err);
@@ -3956,10 +3974,16 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         }
         // dynamic LDS of each kernel at most (k_split_post and k_fin_copy also
         // have static LDS)
-        const std::pair<const void*, int> kernels[8] = {
-            {(const void*)k_align_jobs<true>, (int)LDS_PER_CU},   {(const void*)k_align_sub<true>, (int)LDS_PER_CU},
-            {(const void*)k_align_finish<true>, (int)LDS_PER_CU}, {(const void*)k_align_jobs<false>, (int)LDS_PER_CU},
-            {(const void*)k_align_sub<false>, (int)LDS_PER_CU},   {(const void*)k_align_finish<false>, (int)LDS_PER_CU},
+        const std::pair<const void*, int> kernels[12] = {
+            {(const void*)k_align_jobs<true, SA_WAVES_PER_EU>, (int)LDS_PER_CU},
+            {(const void*)k_align_sub<true, SA_WAVES_PER_EU>, (int)LDS_PER_CU},
+            {(const void*)k_align_jobs<false, SA_WAVES_PER_EU>, (int)LDS_PER_CU},
+            {(const void*)k_align_sub<false, SA_WAVES_PER_EU>, (int)LDS_PER_CU},
+            {(const void*)k_align_jobs<true, SA_WAVES_MANY>, (int)LDS_PER_CU},
+            {(const void*)k_align_sub<true, SA_WAVES_MANY>, (int)LDS_PER_CU},
+            {(const void*)k_align_jobs<false, SA_WAVES_MANY>, (int)LDS_PER_CU},
+            {(const void*)k_align_sub<false, SA_WAVES_MANY>, (int)LDS_PER_CU},
+            {(const void*)k_align_finish<true>, (int)LDS_PER_CU}, {(const void*)k_align_finish<false>, (int)LDS_PER_CU},
             {(const void*)k_split_post, (int)POST_LDS},          {(const void*)k_fin_copy, 32768 * 4}};
         bool lds_ok = true;
         for (const auto& k : kernels)

@@ -25,7 +25,7 @@ if [ "$PART" = tests ]; then
   timeout -k 10 600 python bench.py > $O/bench_c3.log 2>&1 || { tail -5 $O/bench_c3.log; exit 1; }
   tail -1 $O/bench_c3.log | cut -c1-300
 else
-  for cfg in C2 C4 C5; do
+  for cfg in C2 C4 C5 R3; do
     step bench_$cfg
     timeout -k 10 300 python bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-pairs-line > $O/bench_$cfg.log 2>&1 || { tail -5 $O/bench_$cfg.log; exit 1; }
     tail -1 $O/bench_$cfg.log | cut -c1-200

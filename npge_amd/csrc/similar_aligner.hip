@@ -2653,6 +2653,7 @@ struct npgx_aligner {
     int long_head = 128;
     int long_m = 512;
     int long_lds = 1;  // NPGX_LONG_LDS=0: the prefix search on the global word table only (A/B)
+    int64_t waves_many_at = SA_WAVES_MANY_AT;  // NPGX_SA_MANY_AT: tasks past which a launch takes 4 waves a SIMD (A/B)
     // split jobs whose segment rooms for the whole row suffixes take at most
     // this many bytes get them (NPGX_SEG_FULL_MB; 0: the 8-sync-state rooms).
     // R3: the segment overflows (reason 202) go with them; the sub-job
@@ -3188,7 +3189,7 @@ void align_device(npgx_aligner* al, const char* d_rows, const int64_t* row_off, 
         while ((1ull << tlog) < 2ull * (uint64_t)max_n * (uint64_t)(max_len + 1) + 64) tlog++;
         int depth = max_len / std::max(1, o.aligned_check + 1) + 4;
         auto per_slot = [&](uint32_t tl, int dp) { return (20ll << tl) + 1028ll * dp + 17ll * cols_need; };
-        const int wv = nj > SA_WAVES_MANY_AT ? SA_WAVES_MANY : SA_WAVES_PER_EU;  // this launch's waves a SIMD
+        const int wv = nj > al->waves_many_at ? SA_WAVES_MANY : SA_WAVES_PER_EU;  // this launch's waves a SIMD
         size_t slots = (size_t)std::max(1, std::min(nj, 256 * 4 * wv));
         const int64_t mem_budget = std::max<int64_t>(al->slot_budget, 1ll << 22);
         if (attempt == 0)
@@ -3952,6 +3953,8 @@ int npgx_aligner_create(const npgx_align_options* o, npgx_aligner** out) {
         if (lh && *lh) a->long_head = std::max(0, atoi(lh));
         const char* ll = getenv("NPGX_LONG_LDS");
         if (ll && *ll) a->long_lds = atoi(ll) != 0;
+        const char* wm = getenv("NPGX_SA_MANY_AT");
+        if (wm && *wm) a->waves_many_at = std::max(0ll, atoll(wm));
         const char* lm = getenv("NPGX_LONG_M");
         if (lm && *lm) a->long_m = std::max(64, atoi(lm));
         const char* sf = getenv("NPGX_SEG_FULL_MB");

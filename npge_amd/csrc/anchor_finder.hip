@@ -140,7 +140,9 @@ __device__ __forceinline__ bool in_sorted(const uint64_t* v, int64_t n, uint64_t
 // most windows are not in H (C3: 85 %): with linear probing a key whose
 // home slot is empty is absent, and the occupancy bit of the home slot comes
 // from a bit array that stays in cache, so those windows never touch the
-// table's lines
+// table's lines.  (Round 6 measured two alternatives slower: a fingerprint
+// byte per slot, `profiles/r06s_af_fingerprints_ab.txt`, and a second bit
+// array under another hash, r06v: C5 AnchorFinder +4.5 ms.)
 __device__ __forceinline__ int64_t table_find(const TableArgs& t, uint64_t h) {
     uint32_t s = (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> t.shift) & t.mask;
     if (!((t.occ[s >> 5] >> (s & 31)) & 1u)) return -1;
@@ -217,13 +219,12 @@ __device__ __forceinline__ bool bit_in(const uint32_t* __restrict__ P, uint32_t 
 // k_found_collect_f of the same epoch (P does not change in between): one
 // coalesced byte per window instead of kb random P loads there again (P is
 // m/8 bytes: 45 MB at C5, past the L2s, where random loads run at about 55 G/s).
-__global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __restrict__ first,
-                                                      const uint32_t* __restrict__ P) {
-    const Chunk c = a.chunks[blockIdx.x];
+__device__ __forceinline__ void bloom_first_body(const AfArgs& a, uint32_t* first, const uint32_t* P, int64_t bid) {
+    const Chunk c = a.chunks[bid];
     const SeqMeta s = a.meta[c.seq];
     const int64_t p = c.pos + threadIdx.x;
     uint64_t h, dir;
-    uint8_t* wm = a.wmask ? a.wmask + (a.chunk_base + blockIdx.x) * WG + threadIdx.x : nullptr;
+    uint8_t* wm = a.wmask ? a.wmask + (a.chunk_base + bid) * WG + threadIdx.x : nullptr;
     if (!admitted(a, s, p, h, dir)) {
         if (wm) *wm = 0;
         return;
@@ -253,6 +254,10 @@ __global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __rest
         if (!bit_in(P, idx)) atomicMin(&first[idx], ord);
     }
 }
+__global__ __launch_bounds__(WG) void k_bloom_first_f(AfArgs a, uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ P) {
+    bloom_first_body(a, first, P, blockIdx.x);
+}
 
 // found/collect of one epoch, reading P (bits of the earlier epochs) and
 // adding this epoch's bits to Pn (copied to P before the next epoch)
@@ -277,16 +282,13 @@ __device__ __forceinline__ bool found_at_p(const AfArgs& a, const SeqMeta& s, in
     return f;
 }
 
-__global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t* __restrict__ first,
-                                                        const uint32_t* __restrict__ P,
-                                                        uint32_t* __restrict__ Pn,
-                                                        uint64_t* __restrict__ out,
-                                                        unsigned long long* __restrict__ n_out,
-                                                        const uint32_t* __restrict__ P0,
-                                                        unsigned long long* __restrict__ bfirst,
-                                                        unsigned long long* __restrict__ blast) {
+__device__ __forceinline__ void found_collect_body(const AfArgs& a, const uint32_t* first, const uint32_t* P,
+                                                   uint32_t* Pn,  // (may be P: the host's Pw)
+                                                   uint64_t* out, unsigned long long* n_out, const uint32_t* P0,
+                                                   unsigned long long* bfirst, unsigned long long* blast,
+                                                   int64_t bid, int64_t nblk) {
     __shared__ uint8_t fs[WG];
-    const Chunk c = a.chunks[blockIdx.x];
+    const Chunk c = a.chunks[bid];
     const SeqMeta s = a.meta[c.seq];
     const int t = threadIdx.x;
     const int64_t p = c.pos + t;
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
     if (a.wmask) {
         // k_bloom_first_f's admission and P test (kb <= FKB): the first[]
         // entries of the bits outside P are the only random loads left
-        const uint32_t v = a.wmask[(a.chunk_base + blockIdx.x) * WG + t];
+        const uint32_t v = a.wmask[(a.chunk_base + bid) * WG + t];
         if (v & 0x80u) {
             const int64_t w = s.word_off + (p >> 5);
             const int sh = (int)(p & 31) * 2;
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
         uint64_t hp;
         prev = found_at(a, s, p - 1, first, hp);
         col = f && !(a.similar && prev);
-    } else if (bfirst && blockIdx.x == 0 && p > 0) {  // the predecessor is on another rank
+    } else if (bfirst && bid == 0 && p > 0) {  // the predecessor is on another rank
         bfirst[0] = f ? 1ull : 0ull;
         bfirst[1] = h;
         col = false;
@@ -381,15 +383,41 @@ __global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t
         prev = found_at_p(a, s, p - 1, first, P0, hp);
         col = f && !(a.similar && prev);
     }
-    if (blast && blockIdx.x == gridDim.x - 1) {  // the range's last window
+    if (blast && bid == nblk - 1) {  // the range's last window
         const int64_t last = min((int64_t)WG, s.size - a.k + 1 - c.pos) - 1;
         if (t == last) blast[0] = f ? 1ull : 0ull;
     }
     // one of nseg output segments (by global chunk index), each with its own
     // counter on its own 128-byte line: the workgroups' append atomics spread
     // over nseg addresses instead of queueing on one (k_seg_compact packs them)
-    const int64_t seg = (a.chunk_base + blockIdx.x) % a.nseg;
+    const int64_t seg = (a.chunk_base + bid) % a.nseg;
     wg_append(col, h, out + seg * a.seg_cap, n_out + seg * 16);
+}
+__global__ __launch_bounds__(WG) void k_found_collect_f(AfArgs a, const uint32_t* __restrict__ first,
+                                                        const uint32_t* P, uint32_t* Pn,
+                                                        uint64_t* __restrict__ out,
+                                                        unsigned long long* __restrict__ n_out,
+                                                        const uint32_t* __restrict__ P0,
+                                                        unsigned long long* __restrict__ bfirst,
+                                                        unsigned long long* __restrict__ blast) {
+    found_collect_body(a, first, P, Pn, out, n_out, P0, bfirst, blast, blockIdx.x, gridDim.x);
+}
+// One launch for epoch e's found/collect (the first nc workgroups) and epoch
+// e+1's first-setter pass (the rest), with the window masks (P is only read
+// by the first-setter role and only written, by first setters, in the
+// other): a bit the collect role adds to P while the other role runs is
+// either seen there (its first[] is already exact and below every order of
+// epoch e+1) or not (the atomicMin changes nothing, and the mask sends the
+// window to first[], which says the same); and the atomicMins of epoch e+1
+// cannot lower an entry below the order of a window of epoch e that set it.
+// Two launches an epoch become one.
+__global__ __launch_bounds__(WG) void k_bloom_epoch_f(AfArgs ac, AfArgs ab, int64_t nc, uint32_t* first,
+                                                      uint32_t* P, uint64_t* __restrict__ out,
+                                                      unsigned long long* __restrict__ n_out,
+                                                      const uint32_t* __restrict__ P0,
+                                                      unsigned long long* __restrict__ bfirst) {
+    if ((int64_t)blockIdx.x < nc) found_collect_body(ac, first, P, P, out, n_out, P0, bfirst, nullptr, blockIdx.x, nc);
+    else bloom_first_body(ab, first, P, (int64_t)blockIdx.x - nc);
 }
 
 // the segments of found_collect's output, packed in segment order into out;
@@ -923,14 +951,43 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
         // costs two launches and a copy of the m/8-byte bit array; past ~20
         // epochs the filtering gains nothing more: C5 sweep)
         const int auto_epochs = (int)std::min<int64_t>(24, std::max<int64_t>(1, local_windows / (2 << 20)));
+        // With the window masks (kb <= FKB) k_found_collect_f never reads P
+        // and only a bit's first setter adds it: the epoch's new bits go
+        // straight into P (a reader of P in the same launch would need the
+        // bits of the earlier epochs only, but there is none), and the copy
+        // of the m/8-byte array after each epoch goes (C3: 24 x 5 us)
+        uint32_t* Pw = A.wmask ? P : Pn;
         const int64_t per = std::max<int64_t>(
             1, (int64_t)std::ceil(double(nchunks) / std::max(1, af->opt.bloom_epochs > 0 ? af->opt.bloom_epochs
                                                                                           : auto_epochs)));
-        for (int64_t e0 = 0; e0 < nchunks; e0 += per) {
-            const int64_t ne = std::min(per, nchunks - e0);
+        static const bool fuse_env = !(getenv("NPGX_AF_EPOCH_FUSE") && getenv("NPGX_AF_EPOCH_FUSE")[0] == '0');
+        const bool fuse = fuse_env && Pw == P && af->timer.level < 2;  // (NPGX_TIMERS=2 times each pass)
+        auto epoch_args = [&](int64_t e0) {
             AfArgs E = A;
             E.chunks = A.chunks + e0;
             E.chunk_base = e0;
+            return E;
+        };
+        if (fuse) {  // k_bloom_epoch_f: collect of epoch e with the first-setter pass of e + 1
+            hipLaunchKernelGGL(k_bloom_first_f, dim3((unsigned)std::min(per, nchunks)), block, 0, st, epoch_args(0),
+                               af->first.p, P);
+            for (int64_t e0 = 0; e0 < nchunks; e0 += per) {
+                const int64_t ne = std::min(per, nchunks - e0), e1 = e0 + ne;
+                if (e1 < nchunks) {
+                    const int64_t nn = std::min(per, nchunks - e1);
+                    hipLaunchKernelGGL(k_bloom_epoch_f, dim3((unsigned)(ne + nn)), block, 0, st, epoch_args(e0),
+                                       epoch_args(e1), ne, af->first.p, P, af->hseg.p, af->segctr.p, P0,
+                                       e0 == 0 ? bfirst : nullptr);
+                } else {
+                    hipLaunchKernelGGL(k_found_collect_f, dim3((unsigned)ne), block, 0, st, epoch_args(e0), af->first.p,
+                                       P, nullptr, af->hseg.p, af->segctr.p, P0, e0 == 0 ? bfirst : nullptr, blast);
+                }
+                NPGX_HIP(hipGetLastError());
+            }
+        }
+        for (int64_t e0 = 0; e0 < nchunks && !fuse; e0 += per) {
+            const int64_t ne = std::min(per, nchunks - e0);
+            const AfArgs E = epoch_args(e0);
             const dim3 eg((unsigned)ne);
             ti = af->timer.begin("bloom_first", st, 0.0, 0);
             hipLaunchKernelGGL(k_bloom_first_f, eg, block, 0, st, E, af->first.p, P);
@@ -938,12 +995,12 @@ static void af_run(npgx_af* af, const npgx_seqset* ss, const npgx_comm* comm) {
             af->timer.end(ti, st);
             ti = af->timer.begin("found_collect", st, local_windows * (0.375 + 4.0 * kb) * double(ne) / nchunks, 0);
             const bool more = e0 + ne < nchunks;
-            hipLaunchKernelGGL(k_found_collect_f, eg, block, 0, st, E, af->first.p, P, more ? Pn : nullptr,
+            hipLaunchKernelGGL(k_found_collect_f, eg, block, 0, st, E, af->first.p, P, more ? Pw : nullptr,
                                af->hseg.p, af->segctr.p, P0, e0 == 0 ? bfirst : nullptr,
                                more ? nullptr : blast);
             NPGX_HIP(hipGetLastError());
             af->timer.end(ti, st);
-            if (more) NPGX_HIP(hipMemcpyAsync(P, Pn, (size_t)W * 4, hipMemcpyDeviceToDevice, st));
+            if (more && Pw != P) NPGX_HIP(hipMemcpyAsync(P, Pn, (size_t)W * 4, hipMemcpyDeviceToDevice, st));
         }
     } else if (run_local) {
         ti = af->timer.begin("bloom_first", st, 0.0, 0);

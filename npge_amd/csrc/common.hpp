@@ -409,6 +409,7 @@ void align_wide(WideBufs* w, hipStream_t st, const char* d_rows, const int64_t* 
                 double* wait_ms = nullptr);
 void aligner_timer_reset(npgx_aligner* al);
 const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al);
+bool aligner_wants_stats(const npgx_aligner* al);
 void aligner_host_ms(npgx_aligner* al, double* prep, double* wait);  // read and clear
 hipStream_t aligner_stream(const npgx_aligner* al);
 const char* aligner_result(const npgx_aligner* al, const int64_t** row_off);

@@ -3901,6 +3901,7 @@ void aligner_note_epoch(npgx_aligner* al, uint32_t epoch) { al->epoch_base = std
 void aligner_set_long_head(npgx_aligner* al, int32_t long_head) { al->long_head = std::max(0, long_head); }
 int32_t aligner_long_head(const npgx_aligner* al) { return al->long_head; }
 const std::vector<int64_t>& aligner_job_stats(const npgx_aligner* al) { return al->job_stats; }
+bool aligner_wants_stats(const npgx_aligner* al) { return al->want_stats; }
 void aligner_host_ms(npgx_aligner* al, double* prep, double* wait) {
     *prep = al->host_ms[0];
     *wait = al->host_ms[1];

@@ -222,6 +222,8 @@ def main():
     # stage boundaries (markers cost the GPU time: never in the timed region)
     stages = job.stage_timeline()
     stages["ms_per_step"] = round(dt / args.steps * 1e3, 4)
+    if args.anchor_loop:  # (the stage clock splits the DraftPangenome part of the step only)
+        stages["scope"] = "DraftPangenome only: the step's AnchorLoopFast is not split into stages"
     workload = job.workload_name(args.config)
     del job
 
